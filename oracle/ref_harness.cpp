@@ -1,0 +1,137 @@
+// oracle/ref_harness.cpp -- TEST INFRASTRUCTURE ONLY (never shipped, never measured
+// as the product).  Drives the *reference* ReMPI CDC encoder/decoder, compiled from
+// the unmodified sources under /root/reference/src/rempi by oracle/Makefile, so that
+// the C++ restatement (oracle/cdc_oracle.cpp) and the HIP path can be pinned to
+// bytes produced by the reference itself.
+//
+//   ref_cdc encode <in.rec> <out.rempi> <REMPI_MAX>
+//        in.rec = n x 8 x int32 canonical records (rempi_event.h:40-48 layout).
+//        Each record is pushed through rempi_event_list::push (rempi_event_list.cpp:66-99,
+//        run-length merge), then the record loop of rempi_io_thread::write_record
+//        (rempi_io_thread.cpp:56-97) is replayed: extract_encoder_input_format_chunk ->
+//        encode -> write_record_file, then close_record_file (footer,
+//        rempi_encoder_cdc.cpp:2085-2135).  Prints "encode_s <seconds>".
+//   ref_cdc decode <in.rempi> <out.tables>
+//        read_record_file + decode per chunk (rempi_encoder_cdc.cpp:933-1299), dumping the
+//        decoded tables (int64 little-endian, layout in oracle/tables_format.md).
+//        Prints "decode_s <seconds>".
+#include <mpi.h>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstdint>
+#include <vector>
+#include <algorithm>
+#include "rempi_encoder.h"
+#include "rempi_event_list.h"
+#include "rempi_config.h"
+#include "rempi_event.h"
+
+namespace {
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct Dump {
+  FILE* f;
+  void v(int64_t x) { fwrite(&x, sizeof x, 1, f); }
+  template <class Vec> void vec(const Vec& a) {
+    v((int64_t)a.size());
+    for (auto x : a) v((int64_t)x);
+  }
+};
+
+int do_encode(const char* in, const char* out, int max_len) {
+  FILE* f = fopen(in, "rb");
+  if (!f) { perror(in); return 2; }
+  std::vector<int32_t> buf;
+  int32_t r[8];
+  while (fread(r, sizeof r, 1, f) == 1) buf.insert(buf.end(), r, r + 8);
+  fclose(f);
+  size_t n = buf.size() / 8;
+
+  rempi_mode = 0;
+  rempi_gzip = 0;
+  rempi_max_event_length = max_len;
+  rempi_event_list<rempi_event*> events((size_t)1 << 40, 100);
+  for (size_t i = 0; i < n; i++) {
+    const int32_t* q = &buf[8 * i];
+    // create_test_event(event_count, flag, rank, with_next, index, msg_id, matching_id)
+    events.push(rempi_event::create_test_event(q[0], q[2], q[3], q[4], q[5], q[6], q[7]));
+  }
+  events.push_all();
+
+  rempi_encoder_cdc enc(0, out);
+  enc.open_record_file();
+  double t0 = now_s();
+  while (true) {
+    rempi_encoder_input_format* fmt = enc.create_encoder_input_format();
+    if (!enc.extract_encoder_input_format_chunk(events, fmt)) { delete fmt; break; }
+    enc.encode();
+    enc.write_record_file();
+    // The reference's write_queue_vec points into fmt; it is consumed by write_record_file.
+  }
+  enc.close_record_file();
+  double t1 = now_s();
+  printf("encode_s %.6f records %zu\n", t1 - t0, n);
+  return 0;
+}
+
+// rempi_encoder_cdc::decode keeps replay-engine state across chunks and aborts on the
+// second chunk whenever #tables != #epoch ranks (rempi_encoder_cdc.cpp:1262-1267); that
+// state is not part of the decoded data, so the harness clears it before each chunk.
+struct Dec : rempi_encoder_cdc {
+  explicit Dec(const char* p) : rempi_encoder_cdc(1, p) {}
+  void reset_replay_state() { solid_mc_next_clocks_umap_umap.clear(); }
+};
+
+int do_decode(const char* in, const char* out) {
+  rempi_mode = 1;
+  rempi_gzip = 0;
+  Dec dec(in);
+  dec.open_record_file();
+  FILE* f = fopen(out, "wb");
+  if (!f) { perror(out); return 2; }
+  Dump d{f};
+  double total = 0;
+  int64_t chunks = 0;
+  std::vector<rempi_encoder_input_format*> keep;
+  while (true) {
+    rempi_encoder_input_format* fmt = dec.create_encoder_input_format();
+    double t0 = now_s();
+    if (dec.read_record_file(fmt)) { delete fmt; break; }
+    dec.reset_replay_state();
+    dec.decode();
+    total += now_s() - t0;
+    chunks++;
+    d.v((int64_t)fmt->test_tables_map.size());
+    for (auto& kv : fmt->test_tables_map) {
+      rempi_encoder_input_format_test_table* t = kv.second;
+      d.v(kv.first);
+      d.v(t->count);
+      d.vec(t->epoch_rank_vec);
+      d.vec(t->epoch_clock_vec);
+      d.vec(t->with_previous_vec);
+      d.vec(t->matched_index_vec);
+      std::vector<std::pair<size_t, size_t>> um(t->unmatched_events_umap.begin(), t->unmatched_events_umap.end());
+      std::sort(um.begin(), um.end());
+      d.v((int64_t)um.size());
+      for (auto& p : um) { d.v((int64_t)p.first); d.v((int64_t)p.second); }
+      d.vec(t->matched_events_id_vec);
+      d.vec(t->matched_events_delay_vec);
+      d.vec(t->matched_events_permutated_indices_vec);
+    }
+    keep.push_back(fmt);  // decode() hands pointers into fmt to the encoder; keep alive
+  }
+  fclose(f);
+  printf("decode_s %.6f chunks %lld\n", total, (long long)chunks);
+  return 0;
+}
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc >= 5 && std::string(argv[1]) == "encode") return do_encode(argv[2], argv[3], atoi(argv[4]));
+  if (argc >= 4 && std::string(argv[1]) == "decode") return do_decode(argv[2], argv[3]);
+  fprintf(stderr, "usage: ref_cdc encode <in.rec> <out.rempi> <REMPI_MAX> | decode <in.rempi> <out.tables>\n");
+  return 1;
+}

@@ -1,0 +1,118 @@
+"""Random canonical record streams for parity tests (test infrastructure only).
+
+A record is the reference's 8 x int32 test event (rempi_event.h:40-48):
+  [0] event_count [1] type (2 = TEST) [2] flag [3] rank/source [4] with_next
+  [5] index [6] msg_id = Lamport clock [7] matching_set_id
+
+Streams produced here are *canonical*: they are what rempi_event_list::push
+(rempi_event_list.cpp:66-99) hands to the encoder, i.e. no two consecutive records are
+equal in fields 1..7 (the run-length merge has already been applied).  `canonicalize`
+applies that merge to an arbitrary stream.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+TEST = 2
+
+
+def canonicalize(recs: np.ndarray) -> np.ndarray:
+    """rempi_event_list::push merge: a record equal to its predecessor in fields 1..7
+    bumps the predecessor's event_count by one and is dropped (rempi_event_list.cpp:85-89)."""
+    recs = np.asarray(recs, dtype=np.int32).reshape(-1, 8)
+    out = []
+    for r in recs:
+        if out and np.array_equal(out[-1][1:8], r[1:8]):
+            out[-1][0] += 1
+        else:
+            out.append(r.copy())
+    return np.array(out, dtype=np.int32).reshape(-1, 8)
+
+
+def gen_stream(seed: int, n_matched: int, n_sets: int = 2, n_senders: int = 8, jitter: int = 4,
+               p_unmatched: float = 0.2, p_group: float = 0.1, mode: str = "jitter",
+               max_count: int = 63, index_mod: int = 16, rank_base: int = 0,
+               set_ids=None, neg_index: bool = False) -> np.ndarray:
+    """Near-sorted (or adversarial, per `mode`) canonical stream of one rank.
+
+    mode: 'jitter' arrival = clock + U[0, jitter]; 'sorted'; 'reversed' (arrival order is
+    reverse clock order); 'random' (uniformly random arrival order).
+    """
+    rng = np.random.default_rng(seed)
+    if set_ids is None:
+        set_ids = list(range(n_sets))
+    n_senders = max(n_senders, 1)
+    senders = [rank_base + 1 + j for j in range(n_senders)]
+    sender_set = [set_ids[j % len(set_ids)] for j in range(n_senders)]
+    clk = np.full(n_senders, 10, dtype=np.int64)
+    msgs = []  # (arrival_key, tiebreak, src, clock, set)
+    for m in range(n_matched):
+        j = int(rng.integers(n_senders))
+        clk[j] += 1 + int(rng.integers(8))
+        c = int(clk[j])
+        if mode == "jitter":
+            key = c + int(rng.integers(jitter + 1))
+        elif mode == "sorted":
+            key = c
+        elif mode == "reversed":
+            key = -c
+        elif mode == "random":
+            key = int(rng.integers(1 << 30))
+        else:
+            raise ValueError(mode)
+        msgs.append((key, m, senders[j], c, sender_set[j]))
+    msgs.sort()
+    queues = {s: [] for s in set_ids}
+    for k, (_, _, src, c, s) in enumerate(msgs):
+        queues[s].append((k, src, c))
+    heads = {s: 0 for s in set_ids}
+    taken = np.zeros(len(msgs), dtype=bool)
+    recs = []
+    k = 0
+    while k < len(msgs):
+        if taken[k]:
+            k += 1
+            continue
+        s = msgs[k][4]
+        if rng.random() < p_unmatched:
+            cnt = 1 + min(int(rng.geometric(0.5)) - 1, max_count - 1)
+            recs.append([cnt, TEST, 0, 0, 0, 0, 0, s])
+        g = 1
+        if rng.random() < p_group:
+            g = int(rng.integers(2, 5))
+        q = queues[s]
+        members = []
+        while len(members) < g and heads[s] < len(q):
+            kk, src, c = q[heads[s]]
+            heads[s] += 1
+            if taken[kk]:
+                continue
+            taken[kk] = True
+            members.append((src, c))
+        for i, (src, c) in enumerate(members):
+            idx = int(rng.integers(index_mod))
+            if neg_index and rng.random() < 0.05:
+                idx = -1 - idx
+            recs.append([1, TEST, 1, src, 1 if i + 1 < len(members) else 0, idx, c, s])
+        k += 1
+    if rng.random() < p_unmatched:  # trailing poll
+        recs.append([1 + int(rng.integers(5)), TEST, 0, 0, 0, 0, 0, set_ids[0]])
+    return canonicalize(np.array(recs, dtype=np.int32).reshape(-1, 8))
+
+
+def kat_stream() -> np.ndarray:
+    """Known-answer input of test/rempi/rempi_test_compress.cpp:104-113 (rank 1, clocks
+    32,11,17,36,31,12,22,10,16,18) framed as in SURVEY §8(c): 5 polls, the 10 matched
+    receives, 3 polls (already run-length merged)."""
+    recs = [[5, TEST, 0, 0, 0, 0, 0, 0]]
+    for c in [32, 11, 17, 36, 31, 12, 22, 10, 16, 18]:
+        recs.append([1, TEST, 1, 1, 0, 0, c, 0])
+    recs.append([3, TEST, 0, 0, 0, 0, 0, 0])
+    return np.array(recs, dtype=np.int32)
+
+
+def permutation_stream(c, src: int = 1, set_id: int = 0) -> np.ndarray:
+    """A single-table stream whose clock-order permutation is exactly `c`
+    (observed row i carries clock 10 + c[i] from one source)."""
+    recs = [[1, TEST, 1, src, 0, 0, 10 + int(v), set_id] for v in c]
+    return np.array(recs, dtype=np.int32).reshape(-1, 8)
