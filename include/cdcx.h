@@ -1,0 +1,158 @@
+/* cdcx.h -- C ABI of libcdcx.so, the MI355X (gfx950) Clock Delta Compression codec that
+ * drops in behind ReMPI's CDC record writer / replay reader.
+ *
+ * Plain C: pointers, sizes and int status codes only.  Each entry point names the
+ * reference interface it replaces (paths relative to PRUNERS/ReMPI src/rempi/).
+ *
+ * Byte format: identical to rempi_encoder_cdc with REMPI_GZIP=0:
+ *   rank file = ( [size_t payload_len][payload] )* [size_t 0][footer]
+ *   payload   = per matching-set table, ascending set id: int32 set_id, int32 count,
+ *               size_t epoch bytes, size_t ranks[], size_t clocks[], size_t wp_len,
+ *               size_t wp_bytes, size_t LP(with_previous)[], size_t mi_len, size_t mi_bytes,
+ *               size_t matched_index[], size_t uid_bytes, size_t LP(unmatched_id)[],
+ *               size_t ucnt_bytes, size_t unmatched_count[], size_t pair_bytes,
+ *               int32 LP(ids)[], int32 LP(deltas)[]
+ *   footer    = size_t n, int32 ranks[n] (all_epoch_rank_uset order), int32 0
+ *
+ * Input records: the reference's 8 x int32 test event (rempi_event.h:40-48):
+ *   [0] event_count [1] type [2] flag [3] rank [4] with_next [5] index [6] clock
+ *   [7] matching_set_id
+ * as rempi_event_list::push leaves them (consecutive duplicates already merged).
+ * Implementation limit: 0 <= matching_set_id < 256 (REMPI_MAX_RECV_TEST_ID is 128).
+ */
+#ifndef CDCX_H
+#define CDCX_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes.  The reference reports the same conditions with REMPI_ERR
+ * (print + abort, rempi_err.cpp:100-112); the drop-in shim maps non-zero codes to it. */
+#define CDCX_OK 0
+#define CDCX_ERR_ARG 1             /* bad argument */
+#define CDCX_ERR_TRUNCATED_EPOCH 2 /* "The events in this epoch are truncated" (rempi_encoder_cdc.cpp:231) */
+#define CDCX_ERR_CLOCK_ORDER 3     /* "Later message has smaller clock ..." (rempi_encoder_cdc.cpp:251) */
+#define CDCX_ERR_CORRUPT 4         /* "Record data is broken" / inconsistent sizes (:952, :1288) */
+#define CDCX_ERR_HIP 5             /* HIP runtime failure */
+#define CDCX_ERR_LIMIT 6           /* implementation limit (set id range, sources per table) */
+#define CDCX_ERR_NOMEM 7           /* device or host allocation failure */
+
+typedef struct cdcx_opts {
+  int64_t max_event_length; /* REMPI_MAX (rempi_config.cpp:103-108); default 131072 */
+  int32_t gzip;             /* REMPI_GZIP; must be 0 (zlib stage is not on the device path) */
+  int32_t device;           /* HIP device ordinal */
+  int64_t reserved[4];
+} cdcx_opts;
+
+typedef struct cdcx_ctx cdcx_ctx;
+
+/* Replaces `new rempi_encoder_cdc(mode, path)` (rempi_recorder_cdc.cpp:135) for the codec
+ * part: one context per device, reusable across calls, not shared between threads. */
+cdcx_ctx* cdcx_create(const cdcx_opts* opts);
+void cdcx_destroy(cdcx_ctx* ctx);
+/* Human-readable description of the last failure on this context. */
+const char* cdcx_last_error(const cdcx_ctx* ctx);
+/* Releases buffers returned by the host-memory entry points below. */
+void cdcx_free(void* p);
+/* Number of device kernels; name of each (for profiling tables). */
+int cdcx_kernel_count(void);
+const char* cdcx_kernel_name(int k);
+
+/* ---------------------------------------------------------------------------------------
+ * Record side (rempi_io_thread::write_record, rempi_io_thread.cpp:56-97 driving
+ * extract_encoder_input_format_chunk (rempi_encoder_cdc.cpp:740-778), encode (:781-802),
+ * write_record_file (:804-845) and close_record_file/write_footer (:2085-2135)).
+ */
+
+/* Host buffers: encode one rank's whole stream; *out (cdcx_free) receives the complete
+ * rank_<r>.rempi image (chunks, separator, footer). */
+int cdcx_encode_stream(cdcx_ctx* ctx, const int32_t* rec8, size_t n_rec, uint8_t** out,
+                       size_t* out_len);
+
+/* Host buffers: encode exactly one chunk (the records of one
+ * extract_encoder_input_format_chunk call).  *payload (cdcx_free) is what
+ * write_record_file emits after the size_t length; *epoch_ranks (cdcx_free, may be NULL
+ * when n is 0) are the ranks format() inserts into all_epoch_rank_uset, in order. */
+int cdcx_encode_chunk(cdcx_ctx* ctx, const int32_t* rec8, size_t n_rec, uint8_t** payload,
+                      size_t* payload_len, int32_t** epoch_ranks, size_t* n_epoch_ranks);
+
+/* Device-resident batch: n_ranks independent rank streams.
+ *   d_rec    device pointer, records of all ranks concatenated (int32 x 8 each)
+ *   rec_off  host array [n_ranks+1], record offsets of each rank in d_rec
+ * On success *d_out points to a context-owned device buffer holding the n_ranks rank
+ * files; file r is the out_len[r] bytes at out_off[r] (host arrays [n_ranks]; files start
+ * 16-byte aligned).  The buffer stays valid until the next encode call on ctx.
+ * `stream` is a hipStream_t (NULL = default stream). */
+int cdcx_encode_batch_device(cdcx_ctx* ctx, int32_t n_ranks, const int32_t* d_rec,
+                             const int64_t* rec_off, const uint8_t** d_out, int64_t* out_off,
+                             int64_t* out_len, void* stream);
+
+/* After cdcx_encode_batch_device: the clock-sorted (source, clock) keys of every unit
+ * (table within chunk) of the batch, in file order (int32 pairs, context-owned device
+ * buffer).  These are the keys a replaying process receives from the wire; the records
+ * reconstruction below takes them as side input. */
+int cdcx_batch_sorted_keys(cdcx_ctx* ctx, const int32_t** d_keys, int64_t* n_keys);
+
+/* ---------------------------------------------------------------------------------------
+ * Replay side (read_record_file (:933-978), decode (:1016-1299),
+ * cdc_prepare_decode_indices (:1301-1386), read_footer (:2015-2083)).
+ */
+
+/* Host buffers: decode a whole rank file into the int64 table dump of
+ * oracle/tables_format.md (per chunk: table count; per table: set id, count, epoch ranks,
+ * epoch clocks, with_previous, matched_index, unmatched (id,count) sorted by id, ids,
+ * delays, permutated indices).  *dump is released with cdcx_free. */
+int cdcx_decode_stream(cdcx_ctx* ctx, const uint8_t* in, size_t len, uint8_t** dump,
+                       size_t* dump_len);
+
+/* Host buffers: decode a rank file and rebuild each table's observed stream of canonical
+ * records (SURVEY §8(a) decoded-record definition ii).  sorted_keys: per unit, file order,
+ * the clock-sorted {source, clock} pairs.  *rec8 (cdcx_free) gets n_out x 8 int32. */
+int cdcx_reconstruct_stream(cdcx_ctx* ctx, const uint8_t* in, size_t len,
+                            const int32_t* sorted_keys, size_t n_keys, int32_t** rec8,
+                            size_t* n_out);
+
+/* Device-resident batch decode of n_ranks rank files (file r = in_len[r] bytes at
+ * d_in + in_off[r], 8-byte aligned; host arrays) plus records reconstruction from d_keys
+ * (int32 {source, clock} pairs, units in file order; NULL = tables only).  Outputs stay in
+ * context-owned device buffers:
+ *   *d_rec_out  reconstructed records (int32 x 8), units in file order
+ *   *n_rec_out  number of records
+ *   *d_perm     per-unit matched_events_permutated_indices, concatenated (int32) */
+int cdcx_decode_batch_device(cdcx_ctx* ctx, int32_t n_ranks, const uint8_t* d_in,
+                             const int64_t* in_off, const int64_t* in_len,
+                             const int32_t* d_keys, int64_t n_keys,
+                             const int32_t** d_rec_out, int64_t* n_rec_out,
+                             const int32_t** d_perm, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Synthetic workload (definition in DESIGN.md "Synthetic traces"), generated
+ * directly in device memory: n_ranks consecutive ranks starting at first_rank of a job of
+ * world_size ranks, ~events_per_rank records each.  *d_rec (context-owned) and rec_off
+ * (host, [n_ranks+1]) describe the result.  Also available on the host for tests. */
+typedef struct cdcx_gen_params {
+  int32_t world_size;   /* ranks in the job (sources are other ranks) */
+  int32_t senders;      /* senders per rank (capped at world_size-1) */
+  int32_t sets;         /* matching sets per rank */
+  int32_t jitter;       /* arrival jitter J in clock units */
+  int64_t events_per_rank;
+  uint64_t seed_salt;   /* 0 for the reference workload */
+} cdcx_gen_params;
+
+int cdcx_generate_device(cdcx_ctx* ctx, const cdcx_gen_params* p, int32_t first_rank,
+                         int32_t n_ranks, const int32_t** d_rec, int64_t* rec_off, void* stream);
+int cdcx_generate_host(const cdcx_gen_params* p, int32_t rank, int32_t** rec8, size_t* n_rec);
+
+/* Per-kernel device time (ms) accumulated since the last reset, measured with HIP events
+ * on the launch stream when profiling is enabled. */
+int cdcx_set_profiling(cdcx_ctx* ctx, int enabled);
+int cdcx_kernel_times(cdcx_ctx* ctx, double* ms, int64_t* launches, int n);
+int cdcx_reset_kernel_times(cdcx_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CDCX_H */

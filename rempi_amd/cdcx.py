@@ -1,0 +1,307 @@
+"""ctypes binding of libcdcx.so (include/cdcx.h).
+
+This is plumbing for tests and bench.py: every codec byte is produced by the HIP kernels
+behind the C ABI.  Loading fails loudly when the library is missing -- there is no CPU
+fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcdcx.so")
+
+CDCX_OK = 0
+ERRORS = {
+    1: "CDCX_ERR_ARG",
+    2: "CDCX_ERR_TRUNCATED_EPOCH",
+    3: "CDCX_ERR_CLOCK_ORDER",
+    4: "CDCX_ERR_CORRUPT",
+    5: "CDCX_ERR_HIP",
+    6: "CDCX_ERR_LIMIT",
+    7: "CDCX_ERR_NOMEM",
+}
+
+
+class CdcxError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class _Opts(ctypes.Structure):
+    _fields_ = [("max_event_length", ctypes.c_int64), ("gzip", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("reserved", ctypes.c_int64 * 4)]
+
+
+class GenParams(ctypes.Structure):
+    _fields_ = [("world_size", ctypes.c_int32), ("senders", ctypes.c_int32), ("sets", ctypes.c_int32),
+                ("jitter", ctypes.c_int32), ("events_per_rank", ctypes.c_int64), ("seed_salt", ctypes.c_uint64)]
+
+
+P = ctypes.POINTER
+_u8p, _i32p, _i64p, _vp = P(ctypes.c_uint8), P(ctypes.c_int32), P(ctypes.c_int64), ctypes.c_void_p
+
+_SIGNATURES = {
+    "cdcx_create": ([P(_Opts)], _vp),
+    "cdcx_destroy": ([_vp], None),
+    "cdcx_last_error": ([_vp], ctypes.c_char_p),
+    "cdcx_free": ([_vp], None),
+    "cdcx_kernel_count": ([], ctypes.c_int),
+    "cdcx_kernel_name": ([ctypes.c_int], ctypes.c_char_p),
+    "cdcx_encode_stream": ([_vp, _i32p, ctypes.c_size_t, P(_u8p), P(ctypes.c_size_t)], ctypes.c_int),
+    "cdcx_encode_chunk": ([_vp, _i32p, ctypes.c_size_t, P(_u8p), P(ctypes.c_size_t), P(_i32p), P(ctypes.c_size_t)], ctypes.c_int),
+    "cdcx_encode_batch_device": ([_vp, ctypes.c_int32, _vp, _i64p, P(_vp), _i64p, _i64p, _vp], ctypes.c_int),
+    "cdcx_batch_sorted_keys": ([_vp, P(_vp), _i64p], ctypes.c_int),
+    "cdcx_decode_stream": ([_vp, _u8p, ctypes.c_size_t, P(_u8p), P(ctypes.c_size_t)], ctypes.c_int),
+    "cdcx_reconstruct_stream": ([_vp, _u8p, ctypes.c_size_t, _i32p, ctypes.c_size_t, P(_i32p), P(ctypes.c_size_t)], ctypes.c_int),
+    "cdcx_decode_batch_device": ([_vp, ctypes.c_int32, _vp, _i64p, _i64p, _vp, ctypes.c_int64, P(_vp), _i64p, P(_vp), _vp], ctypes.c_int),
+    "cdcx_generate_device": ([_vp, P(GenParams), ctypes.c_int32, ctypes.c_int32, P(_vp), _i64p, _vp], ctypes.c_int),
+    "cdcx_generate_host": ([P(GenParams), ctypes.c_int32, P(_i32p), P(ctypes.c_size_t)], ctypes.c_int),
+    "cdcx_set_profiling": ([_vp, ctypes.c_int], ctypes.c_int),
+    "cdcx_kernel_times": ([_vp, P(ctypes.c_double), _i64p, ctypes.c_int], ctypes.c_int),
+    "cdcx_reset_kernel_times": ([_vp], ctypes.c_int),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libcdcx.so; raises if it is absent (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGNATURES.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGNATURES)
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(P(t))
+
+
+def default_gen_params(world_size=1024, senders=64, sets=4, jitter=8, events_per_rank=10_000_000, seed_salt=0):
+    return GenParams(world_size, senders, sets, jitter, events_per_rank, seed_salt)
+
+
+def generate_host(params: GenParams, rank: int) -> np.ndarray:
+    """Synthetic trace of one rank (host twin of the device generator)."""
+    L = lib()
+    out = _i32p()
+    n = ctypes.c_size_t()
+    rc = L.cdcx_generate_host(ctypes.byref(params), rank, ctypes.byref(out), ctypes.byref(n))
+    if rc:
+        raise CdcxError(rc, "generate_host")
+    arr = np.ctypeslib.as_array(out, shape=(max(n.value, 1) * 8,))[: 8 * n.value].copy().reshape(-1, 8)
+    L.cdcx_free(out)
+    return arr
+
+
+class Context:
+    """One codec context on one HIP device (cdcx_create / cdcx_destroy)."""
+
+    def __init__(self, max_event_length: int = 131072, device: int = 0):
+        L = lib()
+        opts = _Opts(max_event_length, 0, device, (ctypes.c_int64 * 4)())
+        self._c = L.cdcx_create(ctypes.byref(opts))
+        if not self._c:
+            raise CdcxError(5, f"cdcx_create failed (device {device})")
+        self.max_event_length = max_event_length
+
+    def close(self):
+        if getattr(self, "_c", None):
+            lib().cdcx_destroy(self._c)
+            self._c = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != CDCX_OK:
+            raise CdcxError(rc, f"{what}: {lib().cdcx_last_error(self._c).decode(errors='replace')}")
+
+    # -- host-buffer entry points ------------------------------------------------------
+    def encode_stream(self, recs: np.ndarray) -> bytes:
+        L = lib()
+        r = np.ascontiguousarray(recs, dtype=np.int32).reshape(-1, 8)
+        out = _u8p()
+        n = ctypes.c_size_t()
+        self._check(L.cdcx_encode_stream(self._c, _ptr(r, ctypes.c_int32), r.shape[0], ctypes.byref(out), ctypes.byref(n)),
+                    "encode_stream")
+        data = ctypes.string_at(out, n.value)
+        L.cdcx_free(out)
+        return data
+
+    def encode_chunk(self, recs: np.ndarray):
+        L = lib()
+        r = np.ascontiguousarray(recs, dtype=np.int32).reshape(-1, 8)
+        out = _u8p()
+        n = ctypes.c_size_t()
+        er = _i32p()
+        ne = ctypes.c_size_t()
+        self._check(L.cdcx_encode_chunk(self._c, _ptr(r, ctypes.c_int32), r.shape[0], ctypes.byref(out), ctypes.byref(n),
+                                        ctypes.byref(er), ctypes.byref(ne)), "encode_chunk")
+        data = ctypes.string_at(out, n.value)
+        ranks = np.ctypeslib.as_array(er, shape=(max(ne.value, 1),))[: ne.value].copy()
+        L.cdcx_free(out)
+        L.cdcx_free(er)
+        return data, ranks
+
+    def decode_stream(self, data: bytes) -> bytes:
+        L = lib()
+        buf = np.frombuffer(data, dtype=np.uint8).copy()
+        out = _u8p()
+        n = ctypes.c_size_t()
+        self._check(L.cdcx_decode_stream(self._c, _ptr(buf, ctypes.c_uint8), buf.size, ctypes.byref(out), ctypes.byref(n)),
+                    "decode_stream")
+        d = ctypes.string_at(out, n.value)
+        L.cdcx_free(out)
+        return d
+
+    def reconstruct_stream(self, data: bytes, keys: np.ndarray) -> np.ndarray:
+        L = lib()
+        buf = np.frombuffer(data, dtype=np.uint8).copy()
+        k = np.ascontiguousarray(keys, dtype=np.int32).reshape(-1, 2)
+        out = _i32p()
+        n = ctypes.c_size_t()
+        self._check(L.cdcx_reconstruct_stream(self._c, _ptr(buf, ctypes.c_uint8), buf.size, _ptr(k, ctypes.c_int32),
+                                              k.shape[0], ctypes.byref(out), ctypes.byref(n)), "reconstruct_stream")
+        arr = np.ctypeslib.as_array(out, shape=(max(n.value, 1) * 8,))[: 8 * n.value].copy().reshape(-1, 8)
+        L.cdcx_free(out)
+        return arr
+
+    # -- device-resident batch entry points (pointers are device addresses) ----------------
+    def generate_device(self, params: GenParams, first_rank: int, n_ranks: int, stream=None):
+        """-> (device pointer to records, rec_off numpy[n_ranks+1])"""
+        L = lib()
+        d = _vp()
+        off = np.zeros(n_ranks + 1, np.int64)
+        self._check(L.cdcx_generate_device(self._c, ctypes.byref(params), first_rank, n_ranks, ctypes.byref(d),
+                                           _ptr(off, ctypes.c_int64), stream), "generate_device")
+        return d.value, off
+
+    def encode_batch_device(self, d_rec: int, rec_off: np.ndarray, stream=None):
+        """-> (device pointer to output, out_off[n], out_len[n])"""
+        L = lib()
+        n = rec_off.size - 1
+        ro = np.ascontiguousarray(rec_off, dtype=np.int64)
+        d = _vp()
+        oo = np.zeros(n, np.int64)
+        ol = np.zeros(n, np.int64)
+        self._check(L.cdcx_encode_batch_device(self._c, n, d_rec, _ptr(ro, ctypes.c_int64), ctypes.byref(d),
+                                               _ptr(oo, ctypes.c_int64), _ptr(ol, ctypes.c_int64), stream),
+                    "encode_batch_device")
+        return d.value, oo, ol
+
+    def batch_sorted_keys(self):
+        L = lib()
+        d = _vp()
+        n = ctypes.c_int64()
+        self._check(L.cdcx_batch_sorted_keys(self._c, ctypes.byref(d), ctypes.byref(n)), "batch_sorted_keys")
+        return d.value, n.value
+
+    def decode_batch_device(self, d_in: int, in_off: np.ndarray, in_len: np.ndarray, d_keys=None, n_keys=0, stream=None):
+        """-> (device records pointer, n records, device perm pointer)"""
+        L = lib()
+        n = in_off.size
+        oo = np.ascontiguousarray(in_off, dtype=np.int64)
+        ol = np.ascontiguousarray(in_len, dtype=np.int64)
+        dr = _vp()
+        nr = ctypes.c_int64()
+        dp = _vp()
+        self._check(L.cdcx_decode_batch_device(self._c, n, d_in, _ptr(oo, ctypes.c_int64), _ptr(ol, ctypes.c_int64),
+                                               d_keys, n_keys, ctypes.byref(dr), ctypes.byref(nr), ctypes.byref(dp),
+                                               stream), "decode_batch_device")
+        return dr.value, nr.value, dp.value
+
+    # -- profiling -----------------------------------------------------------------------
+    def set_profiling(self, on: bool):
+        self._check(lib().cdcx_set_profiling(self._c, 1 if on else 0), "set_profiling")
+
+    def kernel_times(self):
+        L = lib()
+        k = L.cdcx_kernel_count()
+        ms = (ctypes.c_double * k)()
+        ln = (ctypes.c_int64 * k)()
+        self._check(L.cdcx_kernel_times(self._c, ms, ln, k), "kernel_times")
+        return {L.cdcx_kernel_name(i).decode(): (ms[i], ln[i]) for i in range(k)}
+
+    def reset_kernel_times(self):
+        self._check(lib().cdcx_reset_kernel_times(self._c), "reset_kernel_times")
+
+
+# -- raw device copies for tests/bench (HIP runtime through ctypes) ------------------------
+_hip = None
+
+
+def hip():
+    global _hip
+    if _hip is None:
+        for name in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
+            try:
+                _hip = ctypes.CDLL(name)
+                break
+            except OSError:
+                continue
+        if _hip is None:
+            raise ImportError("libamdhip64.so not found")
+        _hip.hipMemcpy.argtypes = [_vp, _vp, ctypes.c_size_t, ctypes.c_int]
+        _hip.hipMemcpy.restype = ctypes.c_int
+        _hip.hipDeviceSynchronize.restype = ctypes.c_int
+        _hip.hipMalloc.argtypes = [P(_vp), ctypes.c_size_t]
+        _hip.hipMalloc.restype = ctypes.c_int
+        _hip.hipFree.argtypes = [_vp]
+        _hip.hipFree.restype = ctypes.c_int
+    return _hip
+
+
+def d2h(ptr: int, nbytes: int, dtype=np.uint8) -> np.ndarray:
+    out = np.empty(nbytes, dtype=np.uint8)
+    if nbytes:
+        rc = hip().hipMemcpy(out.ctypes.data, ptr, nbytes, 2)  # hipMemcpyDeviceToHost
+        if rc:
+            raise CdcxError(5, f"hipMemcpy D2H failed ({rc})")
+    return out.view(dtype)
+
+
+class DeviceArray:
+    """A hipMalloc'ed copy of a host array (freed on close)."""
+
+    def __init__(self, arr: np.ndarray):
+        a = np.ascontiguousarray(arr)
+        self.nbytes = a.nbytes
+        p = _vp()
+        rc = hip().hipMalloc(ctypes.byref(p), max(self.nbytes, 64))
+        if rc:
+            raise CdcxError(7, f"hipMalloc failed ({rc})")
+        self.ptr = p.value
+        if self.nbytes:
+            rc = hip().hipMemcpy(self.ptr, a.ctypes.data, self.nbytes, 1)  # HostToDevice
+            if rc:
+                raise CdcxError(5, f"hipMemcpy H2D failed ({rc})")
+
+    def close(self):
+        if self.ptr:
+            hip().hipFree(self.ptr)
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,867 @@
+// api.hip -- host orchestration of the CDC kernels and the C ABI of include/cdcx.h.
+//
+// The host side only sequences launches, sizes buffers and lays out offsets; every byte
+// of codec output is produced by the device kernels.  There is no CPU fallback: if the
+// device or a launch fails the call returns CDCX_ERR_HIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/cdcx.h"
+#include "cdcx_kernels.h"
+#include "hash_order.h"
+
+using namespace cdcx;
+
+namespace {
+
+enum KernelId {
+  K_SET_PRESENCE, K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_INC0, K_TILE_SUM, K_RANK_SCAN, K_TILE_P0,
+  K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CHAIN, K_POSITIONS, K_DELTAS,
+  K_WRITE_UNITS, K_CHUNK_HEADERS, K_FOOTER_ORDER, K_FOOTER_WRITE, K_WRITE_KEYS,
+  K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_PERM, K_DEC_RECORDS,
+  K_GEN_TILE_SUMS, K_GEN_RANK_SCAN, K_GEN_FRAMES, K_GEN_AKEYS, K_GEN_ARRIVAL, K_GEN_RECORDS,
+  K_COUNT
+};
+const char* kKernelNames[K_COUNT] = {
+  "k_set_presence", "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_inc0", "k_tile_sum", "k_rank_scan",
+  "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_chain_lane",
+  "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
+  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_lane", "k_dec_records",
+  "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
+
+struct HipError {
+  hipError_t e;
+  const char* what;
+};
+struct CdcxError {
+  int code;
+  std::string msg;
+};
+
+#define HIPCHK(x)                                 \
+  do {                                            \
+    hipError_t e_ = (x);                          \
+    if (e_ != hipSuccess) throw HipError{e_, #x}; \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace
+
+struct cdcx_ctx {
+  int device = 0;
+  int64_t max_len = 131072;
+  std::string err;
+  std::map<std::string, DevBuf> bufs;
+  bool profiling = false;
+  std::vector<double> ktime = std::vector<double>(K_COUNT, 0.0);
+  std::vector<int64_t> klaunch = std::vector<int64_t>(K_COUNT, 0);
+  struct Pending {
+    int kid;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> event_pool;
+  hipStream_t stream = nullptr;
+
+  // results of the last encode
+  uint8_t* d_out = nullptr;
+  int2* d_keys = nullptr;
+  int64_t n_keys = 0;
+  // results of the last decode
+  std::vector<DUnit> dunits;
+  std::vector<DChunk> dchunks;
+  std::vector<int32_t> dfirst_unit, dnunits;
+  int32_t* d_rec_out = nullptr;
+  int64_t n_rec_out = 0;
+  int32_t* d_perm = nullptr;
+  const int32_t* d_gen = nullptr;
+
+  template <class T>
+  T* buf(const std::string& name, size_t count) {
+    DevBuf& b = bufs[name];
+    size_t bytes = std::max<size_t>(count * sizeof(T), 64);
+    if (bytes > b.cap) {
+      if (b.p) HIPCHK(hipFree(b.p));
+      b.p = nullptr;
+      b.cap = 0;
+      size_t want = bytes + bytes / 8;
+      if (hipMalloc(&b.p, want) != hipSuccess) {
+        (void)hipGetLastError();
+        if (hipMalloc(&b.p, bytes) != hipSuccess) {
+          (void)hipGetLastError();
+          throw CdcxError{CDCX_ERR_NOMEM, "device allocation of " + std::to_string(bytes) + " bytes for " + name + " failed"};
+        }
+        want = bytes;
+      }
+      b.cap = want;
+    }
+    return static_cast<T*>(b.p);
+  }
+  void release(const std::string& name) {
+    auto it = bufs.find(name);
+    if (it != bufs.end()) {
+      if (it->second.p) (void)hipFree(it->second.p);
+      bufs.erase(it);
+    }
+  }
+  template <class T>
+  T* upload(const std::string& name, const std::vector<T>& v, hipStream_t s) {
+    T* d = buf<T>(name, v.size());
+    if (!v.empty()) HIPCHK(hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+    return d;
+  }
+  template <class T>
+  std::vector<T> download(const T* d, size_t n, hipStream_t s) {
+    std::vector<T> v(n);
+    if (n) HIPCHK(hipMemcpyAsync(v.data(), d, n * sizeof(T), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return v;
+  }
+  hipEvent_t event() {
+    if (!event_pool.empty()) {
+      hipEvent_t e = event_pool.back();
+      event_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    return e;
+  }
+  template <class K, class... Args>
+  void launch(int kid, K kernel, dim3 g, dim3 b, hipStream_t s, Args... args) {
+    if (g.x == 0 || g.y == 0 || g.z == 0) return;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (profiling) {
+      e0 = event();
+      HIPCHK(hipEventRecord(e0, s));
+    }
+    hipLaunchKernelGGL(kernel, g, b, 0, s, args...);
+    HIPCHK(hipGetLastError());
+    if (profiling) {
+      e1 = event();
+      HIPCHK(hipEventRecord(e1, s));
+      pending.push_back({kid, e0, e1});
+    }
+  }
+  void collect(hipStream_t s) {
+    HIPCHK(hipStreamSynchronize(s));
+    for (auto& p : pending) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+      ktime[p.kid] += ms;
+      klaunch[p.kid]++;
+      event_pool.push_back(p.a);
+      event_pool.push_back(p.b);
+    }
+    pending.clear();
+  }
+  void check_err(uint32_t* d_err, hipStream_t s) {
+    uint32_t e = 0;
+    HIPCHK(hipMemcpyAsync(&e, d_err, 4, hipMemcpyDeviceToHost, s));
+    collect(s);
+    if (e) {
+      for (int code : {CDCX_ERR_TRUNCATED_EPOCH, CDCX_ERR_CLOCK_ORDER, CDCX_ERR_LIMIT, CDCX_ERR_CORRUPT}) {
+        if (e & (1u << code)) {
+          const char* what = code == CDCX_ERR_TRUNCATED_EPOCH ? "The events in this epoch are truncated"
+                             : code == CDCX_ERR_CLOCK_ORDER   ? "Later message has smaller clock than earlier message"
+                             : code == CDCX_ERR_LIMIT         ? "implementation limit exceeded (set id range or sources per table)"
+                                                              : "Record data is broken";
+          throw CdcxError{code, what};
+        }
+      }
+      throw CdcxError{CDCX_ERR_CORRUPT, "device error word " + std::to_string(e)};
+    }
+  }
+};
+
+namespace {
+
+template <class F>
+int guarded(cdcx_ctx* c, F&& f) {
+  if (!c) return CDCX_ERR_ARG;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    f();
+    c->err.clear();
+    return CDCX_OK;
+  } catch (const HipError& e) {
+    c->err = std::string(e.what) + ": " + hipGetErrorString(e.e);
+    c->pending.clear();
+    return CDCX_ERR_HIP;
+  } catch (const CdcxError& e) {
+    c->err = e.msg;
+    c->pending.clear();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    c->err = "host allocation failed";
+    return CDCX_ERR_NOMEM;
+  }
+}
+
+inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+// ---------------------------------------------------------------------------------------
+// Encode a batch of rank streams already in device memory.
+// Outputs: c->d_out with the rank files at file_off[r] (16-aligned), file_len[r].
+void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* rec_off_h, std::vector<int64_t>& file_off,
+                  std::vector<int64_t>& file_len, hipStream_t s) {
+  const int64_t N = rec_off_h[R];
+  const int64_t maxl = c->max_len;
+  std::vector<int64_t> rec_off(rec_off_h, rec_off_h + R + 1), nrec(R);
+  std::vector<Tile> tiles;
+  std::vector<int32_t> tile0(R), ntiles(R);
+  for (int r = 0; r < R; r++) {
+    nrec[r] = rec_off[r + 1] - rec_off[r];
+    if (nrec[r] > INT32_MAX - 2) throw CdcxError{CDCX_ERR_LIMIT, "more than 2^31 records in one rank stream"};
+    tile0[r] = (int32_t)tiles.size();
+    for (int64_t q = 0; q < nrec[r]; q += kTile)
+      tiles.push_back(Tile{r, (int32_t)std::min<int64_t>(kTile, nrec[r] - q), rec_off[r] + q, (int32_t)(q / kTile), 0});
+    ntiles[r] = (int32_t)tiles.size() - tile0[r];
+  }
+  const int64_t NT = (int64_t)tiles.size();
+  int64_t* d_rec_off = c->upload("rec_off", rec_off, s);
+  int64_t* d_nrec = c->upload("nrec", nrec, s);
+  Tile* d_tiles = c->upload("tiles", tiles, s);
+  int32_t* d_tile0 = c->upload("tile0", tile0, s);
+  int32_t* d_ntiles = c->upload("ntiles", ntiles, s);
+  uint32_t* d_err = c->buf<uint32_t>("err", 1);
+  HIPCHK(hipMemsetAsync(d_err, 0, 4, s));
+
+  uint32_t* d_presence = c->buf<uint32_t>("presence", (size_t)R * (kMaxSets / 32));
+  HIPCHK(hipMemsetAsync(d_presence, 0, (size_t)R * (kMaxSets / 32) * 4, s));
+  int16_t* d_dense = c->buf<int16_t>("dense", (size_t)R * kMaxSets);
+  int32_t* d_setlist = c->buf<int32_t>("setlist", (size_t)R * kMaxSets);
+  int32_t* d_nsets = c->buf<int32_t>("nsets", R);
+  uint8_t* d_tix = c->buf<uint8_t>("tix", N);
+  uint32_t* d_hist = c->buf<uint32_t>("hist", NT * kMaxSets);
+  int32_t* d_base = c->buf<int32_t>("base", NT * kMaxSets);
+  int32_t* d_tstart = c->buf<int32_t>("tstart", (size_t)R * (kMaxSets + 1));
+  uint8_t* d_tfirst = c->buf<uint8_t>("tfirst", N);
+  HIPCHK(hipMemsetAsync(d_tfirst, 0, N, s));
+  TRec* d_trec = c->buf<TRec>("trec", N);
+  int32_t* d_t2s = c->buf<int32_t>("t2s", N);
+  uint8_t* d_inc0 = c->buf<uint8_t>("inc0s", N);
+  int32_t* d_tsum = c->buf<int32_t>("tsum", NT);
+  int32_t* d_toff = c->buf<int32_t>("toff", NT);
+  int32_t* d_p0 = c->buf<int32_t>("p0", N + R);
+  std::vector<int64_t> ccap_off(R + 1, 0);
+  for (int r = 0; r < R; r++) ccap_off[r + 1] = ccap_off[r] + nrec[r] / (maxl + 1 > 0 ? maxl + 1 : 1) + 2;
+  int64_t* d_ccap = c->upload("ccap_off", ccap_off, s);
+  int2* d_chunk_cap = c->buf<int2>("chunk_cap", ccap_off[R]);
+  int32_t* d_nchunks = c->buf<int32_t>("nchunks", R);
+
+  c->launch(K_SET_PRESENCE, k_set_presence, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, d_presence, d_err);
+  c->launch(K_SET_DENSE, k_set_dense, dim3(R), dim3(kMaxSets), s, (const uint32_t*)d_presence, d_dense, d_setlist, d_nsets);
+  c->launch(K_TILE_HIST, k_tile_hist, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, (const int16_t*)d_dense, d_tix,
+            d_hist);
+  c->launch(K_HIST_SCAN, k_hist_scan, dim3(R), dim3(256), s, (const uint32_t*)d_hist, (const int32_t*)d_tile0,
+            (const int32_t*)d_ntiles, (const int32_t*)d_nsets, (const int64_t*)d_rec_off, d_base, d_tstart, d_tfirst);
+  c->launch(K_SCATTER, k_scatter, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, (const uint8_t*)d_tix,
+            (const int32_t*)d_base, (const int64_t*)d_rec_off, d_trec, d_t2s);
+  c->launch(K_INC0, k_inc0, dim3(NT), dim3(256), s, (const TRec*)d_trec, (const int32_t*)d_t2s, (const uint8_t*)d_tfirst,
+            (const Tile*)d_tiles, (const int64_t*)d_rec_off, d_inc0);
+  c->launch(K_TILE_SUM, k_tile_sum, dim3(NT), dim3(256), s, (const uint8_t*)d_inc0, (const Tile*)d_tiles, d_tsum);
+  c->launch(K_RANK_SCAN, k_rank_scan, dim3(R), dim3(256), s, (const int32_t*)d_tsum, (const int32_t*)d_tile0,
+            (const int32_t*)d_ntiles, d_toff);
+  c->launch(K_TILE_P0, k_tile_p0, dim3(NT), dim3(256), s, (const uint8_t*)d_inc0, (const Tile*)d_tiles,
+            (const int32_t*)d_toff, (const int64_t*)d_rec_off, (const int64_t*)d_nrec, d_p0);
+  c->launch(K_CHUNKS, k_chunks, dim3(R), dim3(64), s, d_rec, (const int64_t*)d_rec_off, (const int64_t*)d_nrec,
+            (const int32_t*)d_p0, (const uint8_t*)d_inc0, (const int32_t*)d_t2s, (const int32_t*)d_tstart,
+            (const int32_t*)d_nsets, (const int64_t*)d_ccap, maxl, d_chunk_cap, d_nchunks);
+  c->check_err(d_err, s);
+  std::vector<int32_t> nsets = c->download(d_nsets, R, s);
+  std::vector<int32_t> setlist = c->download(d_setlist, (size_t)R * kMaxSets, s);
+  std::vector<int32_t> nchunks = c->download(d_nchunks, R, s);
+  std::vector<int2> chunk_cap = c->download(d_chunk_cap, ccap_off[R], s);
+
+  // Chunks and units (host bookkeeping over a few thousand entries).
+  std::vector<Chunk> chunks;
+  std::vector<int64_t> lb_off;
+  int64_t lbn = 0;
+  for (int r = 0; r < R; r++) {
+    for (int k = 0; k < nchunks[r]; k++) {
+      const int2 se = chunk_cap[ccap_off[r] + k];
+      chunks.push_back(Chunk{r, se.x, se.y, 0, 0, 0, 0, 0});
+      lb_off.push_back(lbn);
+      lbn += nsets[r];
+    }
+  }
+  const int32_t C = (int32_t)chunks.size();
+  Chunk* d_chunks = c->upload("chunks", chunks, s);
+  int64_t* d_lb_off = c->upload("lb_off", lb_off, s);
+  int2* d_lohi = c->buf<int2>("lohi", lbn);
+  c->launch(K_UNITS_LB, k_units_lb, dim3(C), dim3(256), s, (const Chunk*)d_chunks, C, (const int64_t*)d_lb_off,
+            (const int32_t*)d_nsets, (const int32_t*)d_tstart, (const int64_t*)d_rec_off, (const int32_t*)d_t2s, d_lohi);
+  std::vector<int2> lohi = c->download(d_lohi, lbn, s);
+  std::vector<Unit> units;
+  std::vector<int64_t> w1;
+  int64_t w1n = 0;
+  std::vector<int32_t> ufirst(R, 0), nunits(R, 0);
+  for (int32_t ci = 0; ci < C; ci++) {
+    Chunk& ch = chunks[ci];
+    ch.first_unit = (int32_t)units.size();
+    if (ci == 0 || chunks[ci - 1].rank != ch.rank) ufirst[ch.rank] = ch.first_unit;
+    for (int t = 0; t < nsets[ch.rank]; t++) {
+      const int2 lh = lohi[lb_off[ci] + t];
+      if (lh.y <= lh.x) continue;
+      Unit u{};
+      u.a = rec_off[ch.rank] + lh.x;
+      u.n = lh.y - lh.x;
+      u.rank = ch.rank;
+      u.chunk = ci;
+      u.set_id = setlist[(size_t)ch.rank * kMaxSets + t];
+      units.push_back(u);
+      w1.push_back(w1n);
+      w1n += u.n + 1;
+    }
+    ch.n_units = (int32_t)units.size() - ch.first_unit;
+    nunits[ch.rank] += ch.n_units;
+  }
+  const int32_t NU = (int32_t)units.size();
+  Unit* d_units = c->upload("units", units, s);
+  int64_t* d_w1 = c->upload("w1", w1, s);
+  uint64_t* d_mkey = c->buf<uint64_t>("mkey", N);
+  int32_t* d_midx = c->buf<int32_t>("midx", N);
+  int32_t* d_wp = c->buf<int32_t>("wp", N);
+  int32_t* d_run_id = c->buf<int32_t>("run_id", N);
+  uint64_t* d_run_cnt = c->buf<uint64_t>("run_cnt", N);
+  c->launch(K_UNIT_PREP, k_unit_prep, dim3(NU), dim3(256), s, d_units, (const TRec*)d_trec, d_mkey, d_midx, d_wp, d_run_id,
+            d_run_cnt, d_err);
+  c->check_err(d_err, s);
+  units = c->download(d_units, NU, s);
+
+  // Sort tiles.
+  std::vector<SortTile> st;
+  for (int32_t u = 0; u < NU; u++) {
+    units[u].sort_tile0 = (int32_t)st.size();
+    for (int32_t q = 0; q * kSortTile < units[u].M; q++) st.push_back(SortTile{u, q});
+  }
+  const int64_t NS = (int64_t)st.size();
+  d_units = c->upload("units", units, s);
+  SortTile* d_st = c->upload("sort_tiles", st, s);
+  uint64_t* d_tkey = c->buf<uint64_t>("tkey", N);
+  int32_t* d_lrank = c->buf<int32_t>("lrank", N);
+  uint64_t* d_tmm = c->buf<uint64_t>("tminmax", 2 * NS);
+  int32_t* d_cord = c->buf<int32_t>("cord", N);
+  int32_t* d_inv = c->buf<int32_t>("inv", N);
+  uint64_t* d_skey = c->buf<uint64_t>("skey", N);
+  c->launch(K_SORT_TILES, k_sort_tiles, dim3(NS), dim3(256), s, (const Unit*)d_units, (const SortTile*)d_st,
+            (const uint64_t*)d_mkey, d_tkey, d_lrank, d_tmm);
+  c->launch(K_RANK_TILES, k_rank_tiles, dim3(NS), dim3(256), s, (const Unit*)d_units, (const SortTile*)d_st,
+            (const uint64_t*)d_mkey, (const uint64_t*)d_tkey, (const int32_t*)d_lrank, (const uint64_t*)d_tmm, d_cord,
+            d_inv, d_skey);
+  uint64_t* d_ep_rank = c->buf<uint64_t>("ep_rank", N);
+  uint64_t* d_ep_clk = c->buf<uint64_t>("ep_clk", N);
+  c->launch(K_EPOCH, k_epoch, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, d_err);
+  int32_t* d_par = c->buf<int32_t>("par", N);
+  int32_t* d_lvl = c->buf<int32_t>("lvl", N);
+  int32_t* d_leaves = c->buf<int32_t>("leaves", w1n);
+  uint8_t* d_chain = c->buf<uint8_t>("chain", N);
+  HIPCHK(hipMemsetAsync(d_chain, 0, N, s));
+  c->launch(K_CHAIN, k_chain_lane, dim3(blocks(NU, 64)), dim3(64), s, d_units, NU, (const int32_t*)d_cord,
+            (const int32_t*)d_inv, d_par, d_lvl, d_leaves, (const int64_t*)d_w1, d_chain);
+  int32_t* d_posA = c->buf<int32_t>("posA", N);
+  int32_t* d_posR = c->buf<int32_t>("posR", N);
+  uint32_t* d_seq = c->buf<uint32_t>("seq", 2 * N);
+  int32_t* d_sidx = c->buf<int32_t>("sidx", 2 * N);
+  c->launch(K_POSITIONS, k_positions, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_cord,
+            (const int32_t*)d_inv, (const uint8_t*)d_chain, d_posA, d_posR, d_seq, d_sidx);
+  int32_t* d_pid = c->buf<int32_t>("pid", N);
+  int32_t* d_pdl = c->buf<int32_t>("pdl", N);
+  c->launch(K_DELTAS, k_deltas, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_cord,
+            (const uint8_t*)d_chain, (const int32_t*)d_posA, (const int32_t*)d_posR, (const uint32_t*)d_seq,
+            (const int32_t*)d_sidx, d_pid, d_pdl);
+  c->check_err(d_err, s);
+  units = c->download(d_units, NU, s);
+
+  // Sizes, footer scratch, offsets.
+  std::vector<int64_t> fk_off(R + 1, 0), fb_off(R + 1, 0);
+  {
+    std::vector<int64_t> bound(R, 0);
+    for (const Unit& u : units) bound[u.rank] += u.S;
+    for (int r = 0; r < R; r++) {
+      fk_off[r + 1] = fk_off[r] + bound[r] + 1;
+      fb_off[r + 1] = fb_off[r] + (int64_t)hash_bucket_capacity((uint64_t)bound[r]) + 1;
+    }
+  }
+  int64_t key_run = 0;
+  for (Unit& u : units) {
+    u.key_off = key_run;
+    key_run += u.M;
+  }
+  d_units = c->upload("units", units, s);
+  int32_t* d_ufirst = c->upload("ufirst", ufirst, s);
+  int32_t* d_nunits = c->upload("nunits", nunits, s);
+  int64_t* d_fk_off = c->upload("fk_off", fk_off, s);
+  int64_t* d_fb_off = c->upload("fb_off", fb_off, s);
+  uint64_t* d_fkey = c->buf<uint64_t>("fkey", fk_off[R]);
+  int32_t* d_fnext = c->buf<int32_t>("fnext", fk_off[R]);
+  int32_t* d_fbucket = c->buf<int32_t>("fbucket", fb_off[R]);
+  int32_t* d_fcount = c->buf<int32_t>("fcount", R);
+  c->launch(K_FOOTER_ORDER, k_footer_order, dim3(blocks(R, 64)), dim3(64), s, (const Unit*)d_units,
+            (const int32_t*)d_ufirst, (const int32_t*)d_nunits, (const uint64_t*)d_ep_rank, R, (const int64_t*)d_fk_off,
+            (const int64_t*)d_fb_off, d_fkey, d_fnext, d_fbucket, d_fcount);
+  std::vector<int32_t> fcount = c->download(d_fcount, R, s);
+
+  file_off.assign(R, 0);
+  file_len.assign(R, 0);
+  std::vector<int64_t> foot_off(R, 0);
+  int64_t pos = 0;
+  size_t ui = 0;
+  int32_t ci = 0;
+  for (int r = 0; r < R; r++) {
+    pos = align_up(pos, 16);
+    file_off[r] = pos;
+    for (; ci < C && chunks[ci].rank == r; ci++) {
+      Chunk& ch = chunks[ci];
+      ch.out_off = pos;
+      int64_t q = pos + 8;
+      for (int32_t k = 0; k < ch.n_units; k++, ui++) {
+        Unit& u = units[ui];
+        u.out_off = q;
+        q += 72 + 16ll * u.S + 8ll * u.W + 8ll * u.M + 16ll * u.U + 8ll * u.P;
+      }
+      ch.payload = q - pos - 8;
+      pos = q;
+    }
+    foot_off[r] = pos;
+    pos += 20 + 4ll * fcount[r];
+    file_len[r] = pos - file_off[r];
+  }
+  const int64_t total = align_up(pos, 16);
+  d_units = c->upload("units", units, s);
+  d_chunks = c->upload("chunks", chunks, s);
+  int64_t* d_foot = c->upload("foot_off", foot_off, s);
+  uint8_t* d_out = c->buf<uint8_t>("out", total);
+  int2* d_keys = c->buf<int2>("keys", key_run);
+  c->launch(K_WRITE_UNITS, k_write_units, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_midx,
+            (const int32_t*)d_wp, (const int32_t*)d_run_id, (const uint64_t*)d_run_cnt, (const uint64_t*)d_ep_rank,
+            (const uint64_t*)d_ep_clk, (const int32_t*)d_pid, (const int32_t*)d_pdl, d_out);
+  c->launch(K_CHUNK_HEADERS, k_chunk_headers, dim3(blocks(C, 256)), dim3(256), s, (const Chunk*)d_chunks, C, d_out);
+  c->launch(K_FOOTER_WRITE, k_footer_write, dim3(blocks(R, 64)), dim3(64), s, (const int64_t*)d_fk_off,
+            (const int64_t*)d_fb_off, (const uint64_t*)d_fkey, (const int32_t*)d_fnext, (const int32_t*)d_fbucket,
+            (const int32_t*)d_fcount, (const int64_t*)d_foot, R, d_out);
+  c->launch(K_WRITE_KEYS, k_write_keys, dim3(NU), dim3(256), s, (const Unit*)d_units, (const uint64_t*)d_skey, d_keys);
+  c->check_err(d_err, s);
+  c->d_out = d_out;
+  c->d_keys = d_keys;
+  c->n_keys = key_run;
+}
+
+// ---------------------------------------------------------------------------------------
+// Decode a batch of rank files in device memory (d_in; file r at off[r], len[r], 8-aligned).
+void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector<int64_t>& off,
+                  const std::vector<int64_t>& len, const int2* d_keys, int64_t n_keys, bool records, hipStream_t s) {
+  for (int r = 0; r < R; r++)
+    if (off[r] & 7) throw CdcxError{CDCX_ERR_ARG, "rank files must start 8-byte aligned"};
+  int64_t* d_off = c->upload("d_off", off, s);
+  int64_t* d_len = c->upload("d_len", len, s);
+  uint32_t* d_err = c->buf<uint32_t>("err", 1);
+  HIPCHK(hipMemsetAsync(d_err, 0, 4, s));
+  int32_t* d_nch = c->buf<int32_t>("d_nchunks", R);
+  c->launch(K_DEC_COUNT_CHUNKS, k_dec_count_chunks, dim3(blocks(R, 64)), dim3(64), s, d_in, (const int64_t*)d_off,
+            (const int64_t*)d_len, R, d_nch, d_err);
+  c->check_err(d_err, s);
+  std::vector<int32_t> nch = c->download(d_nch, R, s), cbase(R, 0);
+  int32_t C = 0;
+  for (int r = 0; r < R; r++) {
+    cbase[r] = C;
+    C += nch[r];
+  }
+  int32_t* d_cbase = c->upload("d_cbase", cbase, s);
+  DChunk* d_ch = c->buf<DChunk>("d_chunks", C);
+  c->launch(K_DEC_LIST_CHUNKS, k_dec_list_chunks, dim3(blocks(R, 64)), dim3(64), s, d_in, (const int64_t*)d_off,
+            (const int32_t*)d_cbase, (const int32_t*)d_nch, R, d_ch);
+  int32_t* d_nu = c->buf<int32_t>("d_nunits", C);
+  c->launch(K_DEC_UNITS, k_dec_units, dim3(blocks(C, 64)), dim3(64), s, d_in, (const DChunk*)d_ch, C,
+            (const int32_t*)nullptr, d_nu, (DUnit*)nullptr, d_err);
+  c->check_err(d_err, s);
+  c->dnunits = c->download(d_nu, C, s);
+  c->dfirst_unit.assign(C, 0);
+  int32_t NU = 0;
+  for (int32_t k = 0; k < C; k++) {
+    c->dfirst_unit[k] = NU;
+    NU += c->dnunits[k];
+  }
+  int32_t* d_fu = c->upload("d_first_unit", c->dfirst_unit, s);
+  DUnit* d_units = c->buf<DUnit>("d_units", NU);
+  c->launch(K_DEC_UNITS, k_dec_units, dim3(blocks(C, 64)), dim3(64), s, d_in, (const DChunk*)d_ch, C, (const int32_t*)d_fu,
+            (int32_t*)nullptr, d_units, d_err);
+  c->check_err(d_err, s);
+  c->dchunks = c->download(d_ch, C, s);
+  std::vector<DUnit> units = c->download(d_units, NU, s);
+  int64_t wb = 0, ro = 0, ko = 0;
+  for (DUnit& u : units) {
+    u.wbase = wb;
+    u.rec_off = ro;
+    u.key_off = ko;
+    wb += (int64_t)u.M + 1;
+    ro += (int64_t)u.M + (u.Uc > 0 ? u.U : 0);
+    ko += u.M;
+  }
+  if (records && n_keys < ko) throw CdcxError{CDCX_ERR_ARG, "fewer sorted keys than matched events in the files"};
+  d_units = c->upload("d_units", units, s);
+  c->dunits = units;
+  uint64_t* d_wpd = c->buf<uint64_t>("d_wpd", wb);
+  uint64_t* d_uidd = c->buf<uint64_t>("d_uidd", wb);
+  uint64_t* d_idd = c->buf<uint64_t>("d_idd", wb);
+  uint64_t* d_dld = c->buf<uint64_t>("d_dld", wb);
+  int32_t* d_nx = c->buf<int32_t>("d_nx", wb);
+  int32_t* d_pv = c->buf<int32_t>("d_pv", wb);
+  int32_t* d_perm = c->buf<int32_t>("d_perm", ko);
+  c->launch(K_DEC_SECTIONS, k_dec_sections, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, d_wpd, d_uidd, d_idd, d_dld);
+  c->launch(K_DEC_PERM, k_dec_perm_lane, dim3(blocks(NU, 64)), dim3(64), s, (const DUnit*)d_units, NU,
+            (const uint64_t*)d_idd, (const uint64_t*)d_dld, d_nx, d_pv, d_perm, d_err);
+  c->check_err(d_err, s);
+  c->d_perm = d_perm;
+  c->n_rec_out = ro;
+  if (records) {
+    int32_t* d_cinv = c->buf<int32_t>("d_cinv", wb);
+    uint8_t* d_wnf = c->buf<uint8_t>("d_wnf", wb);
+    int32_t* d_recs = c->buf<int32_t>("d_recs", 8 * ro);
+    c->launch(K_DEC_RECORDS, k_dec_records, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, (const int32_t*)d_perm,
+              (const uint64_t*)d_wpd, (const uint64_t*)d_uidd, d_keys, d_cinv, d_wnf, (int4*)d_recs, d_err);
+    c->check_err(d_err, s);
+    c->d_rec_out = d_recs;
+  }
+}
+
+// Host-side table dump of the last decode (tests / drop-in shim): mirrors the fields the
+// reference keeps in rempi_encoder_input_format_test_table after decode().
+std::vector<int64_t> tables_dump(cdcx_ctx* c, const uint8_t* in, hipStream_t s) {
+  const size_t NU = c->dunits.size();
+  int64_t wb = 0, ko = 0;
+  for (auto& u : c->dunits) { wb = std::max(wb, u.wbase + u.M + 1); ko = std::max(ko, u.key_off + u.M); }
+  std::vector<uint64_t> wpd = c->download(c->buf<uint64_t>("d_wpd", 0), wb, s);
+  std::vector<uint64_t> uidd = c->download(c->buf<uint64_t>("d_uidd", 0), wb, s);
+  std::vector<uint64_t> idd = c->download(c->buf<uint64_t>("d_idd", 0), wb, s);
+  std::vector<uint64_t> dld = c->download(c->buf<uint64_t>("d_dld", 0), wb, s);
+  std::vector<int32_t> perm = c->download(c->d_perm, ko, s);
+  (void)NU;
+  std::vector<int64_t> d;
+  auto u64at = [&](int64_t o) {
+    uint64_t v;
+    memcpy(&v, in + o, 8);
+    return (int64_t)v;
+  };
+  for (size_t k = 0; k < c->dchunks.size(); k++) {
+    std::map<int32_t, int32_t> bysid;  // test_tables_map: last table with an id wins
+    for (int32_t q = 0; q < c->dnunits[k]; q++) bysid[c->dunits[c->dfirst_unit[k] + q].set_id] = c->dfirst_unit[k] + q;
+    d.push_back((int64_t)bysid.size());
+    for (auto& kv : bysid) {
+      const DUnit& u = c->dunits[kv.second];
+      d.push_back(u.set_id);
+      d.push_back(u.M);
+      d.push_back(u.S);
+      for (int32_t i = 0; i < u.S; i++) d.push_back(u64at(u.ep_off + 8ll * i));
+      d.push_back(u.S);
+      for (int32_t i = 0; i < u.S; i++) d.push_back(u64at(u.ep_off + 8ll * (u.S + i)));
+      d.push_back(u.W);
+      for (int32_t i = 0; i < u.W; i++) d.push_back((int64_t)wpd[u.wbase + i]);
+      d.push_back(u.Mi);
+      for (int32_t i = 0; i < u.Mi; i++) d.push_back(u64at(u.mi_off + 8ll * i));
+      std::map<uint64_t, uint64_t> um;
+      if (u.Uc > 0)
+        for (int32_t i = 0; i < u.U; i++) um[uidd[u.wbase + i]] = (uint64_t)u64at(u.ucnt_off + 8ll * i);
+      d.push_back((int64_t)um.size());
+      for (auto& p : um) {
+        d.push_back((int64_t)p.first);
+        d.push_back((int64_t)p.second);
+      }
+      d.push_back(u.P);
+      for (int32_t i = 0; i < u.P; i++) d.push_back((int64_t)idd[u.wbase + i]);
+      d.push_back(u.P);
+      for (int32_t i = 0; i < u.P; i++) d.push_back((int64_t)dld[u.wbase + i]);
+      d.push_back(u.M);
+      for (int32_t i = 0; i < u.M; i++) d.push_back(perm[u.key_off + i]);
+    }
+  }
+  return d;
+}
+
+template <class T>
+T* host_copy(const std::vector<T>& v) {
+  T* p = static_cast<T*>(malloc(std::max<size_t>(v.size() * sizeof(T), 1)));
+  if (!p) throw std::bad_alloc();
+  if (!v.empty()) memcpy(p, v.data(), v.size() * sizeof(T));
+  return p;
+}
+
+}  // namespace
+
+// =========================================================================================
+extern "C" {
+
+cdcx_ctx* cdcx_create(const cdcx_opts* opts) {
+  cdcx_ctx* c = new (std::nothrow) cdcx_ctx();
+  if (!c) return nullptr;
+  if (opts) {
+    c->device = opts->device;
+    if (opts->max_event_length > 0) c->max_len = opts->max_event_length;
+    if (opts->gzip != 0) {
+      delete c;
+      return nullptr;
+    }
+  }
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || c->device < 0 || c->device >= n || hipSetDevice(c->device) != hipSuccess) {
+    (void)hipGetLastError();
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
+void cdcx_destroy(cdcx_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  for (auto& kv : c->bufs)
+    if (kv.second.p) (void)hipFree(kv.second.p);
+  for (auto e : c->event_pool) (void)hipEventDestroy(e);
+  for (auto& p : c->pending) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  delete c;
+}
+
+const char* cdcx_last_error(const cdcx_ctx* c) { return c ? c->err.c_str() : "null context"; }
+void cdcx_free(void* p) { free(p); }
+int cdcx_kernel_count(void) { return K_COUNT; }
+const char* cdcx_kernel_name(int k) { return (k >= 0 && k < K_COUNT) ? kKernelNames[k] : ""; }
+
+int cdcx_encode_batch_device(cdcx_ctx* c, int32_t n_ranks, const int32_t* d_rec, const int64_t* rec_off,
+                             const uint8_t** d_out, int64_t* out_off, int64_t* out_len, void* stream) {
+  if (!c || n_ranks <= 0 || !rec_off || !d_out || !out_off || !out_len) return CDCX_ERR_ARG;
+  return guarded(c, [&] {
+    std::vector<int64_t> fo, fl;
+    encode_batch(c, n_ranks, d_rec, rec_off, fo, fl, (hipStream_t)stream);
+    *d_out = c->d_out;
+    std::copy(fo.begin(), fo.end(), out_off);
+    std::copy(fl.begin(), fl.end(), out_len);
+  });
+}
+
+int cdcx_batch_sorted_keys(cdcx_ctx* c, const int32_t** d_keys, int64_t* n_keys) {
+  if (!c || !d_keys || !n_keys) return CDCX_ERR_ARG;
+  *d_keys = reinterpret_cast<const int32_t*>(c->d_keys);
+  *n_keys = c->n_keys;
+  return CDCX_OK;
+}
+
+int cdcx_encode_stream(cdcx_ctx* c, const int32_t* rec8, size_t n, uint8_t** out, size_t* out_len) {
+  if (!c || (n && !rec8) || !out || !out_len) return CDCX_ERR_ARG;
+  return guarded(c, [&] {
+    hipStream_t s = c->stream;
+    int32_t* d = c->buf<int32_t>("h_in", 8 * n);
+    if (n) HIPCHK(hipMemcpyAsync(d, rec8, 32 * n, hipMemcpyHostToDevice, s));
+    int64_t ro[2] = {0, (int64_t)n};
+    std::vector<int64_t> fo, fl;
+    encode_batch(c, 1, d, ro, fo, fl, s);
+    std::vector<uint8_t> h(fl[0]);
+    HIPCHK(hipMemcpyAsync(h.data(), c->d_out + fo[0], fl[0], hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    *out = host_copy(h);
+    *out_len = h.size();
+  });
+}
+
+int cdcx_encode_chunk(cdcx_ctx* c, const int32_t* rec8, size_t n, uint8_t** payload, size_t* payload_len,
+                      int32_t** epoch_ranks, size_t* n_epoch_ranks) {
+  if (!c || (n && !rec8) || !payload || !payload_len || !epoch_ranks || !n_epoch_ranks) return CDCX_ERR_ARG;
+  const int64_t saved = c->max_len;
+  c->max_len = INT64_MAX / 4;
+  int rc = guarded(c, [&] {
+    hipStream_t s = c->stream;
+    std::vector<uint8_t> h;
+    if (n) {
+      int32_t* d = c->buf<int32_t>("h_in", 8 * n);
+      HIPCHK(hipMemcpyAsync(d, rec8, 32 * n, hipMemcpyHostToDevice, s));
+      int64_t ro[2] = {0, (int64_t)n};
+      std::vector<int64_t> fo, fl;
+      encode_batch(c, 1, d, ro, fo, fl, s);
+      h.resize(fl[0]);
+      HIPCHK(hipMemcpyAsync(h.data(), c->d_out + fo[0], fl[0], hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
+    std::vector<uint8_t> pl;
+    std::vector<int32_t> er;
+    if (!h.empty()) {
+      uint64_t plen;
+      memcpy(&plen, h.data(), 8);
+      pl.assign(h.begin() + 8, h.begin() + 8 + plen);
+      // epoch ranks in table order, as format() inserts them (rempi_encoder_cdc.cpp:261-267)
+      size_t q = 0;
+      while (q < pl.size()) {
+        uint64_t esz;
+        memcpy(&esz, &pl[q + 8], 8);
+        for (uint64_t i = 0; i < esz / 8; i++) {
+          uint64_t v;
+          memcpy(&v, &pl[q + 16 + 8 * i], 8);
+          er.push_back((int32_t)v);
+        }
+        size_t p = q + 16 + 2 * esz;
+        uint64_t w;
+        memcpy(&w, &pl[p + 8], 8);
+        p += 16 + w;
+        memcpy(&w, &pl[p + 8], 8);
+        p += 16 + w;
+        memcpy(&w, &pl[p], 8);
+        p += 8 + w;
+        memcpy(&w, &pl[p], 8);
+        p += 8 + w;
+        memcpy(&w, &pl[p], 8);
+        p += 8 + w;
+        q = p;
+      }
+    }
+    *payload = host_copy(pl);
+    *payload_len = pl.size();
+    *epoch_ranks = host_copy(er);
+    *n_epoch_ranks = er.size();
+  });
+  c->max_len = saved;
+  return rc;
+}
+
+int cdcx_decode_stream(cdcx_ctx* c, const uint8_t* in, size_t len, uint8_t** dump, size_t* dump_len) {
+  if (!c || (len && !in) || !dump || !dump_len) return CDCX_ERR_ARG;
+  return guarded(c, [&] {
+    hipStream_t s = c->stream;
+    uint8_t* d = c->buf<uint8_t>("h_file", len);
+    if (len) HIPCHK(hipMemcpyAsync(d, in, len, hipMemcpyHostToDevice, s));
+    decode_batch(c, 1, d, {0}, {(int64_t)len}, nullptr, 0, false, s);
+    std::vector<int64_t> t = tables_dump(c, in, s);
+    *dump = reinterpret_cast<uint8_t*>(host_copy(t));
+    *dump_len = t.size() * 8;
+  });
+}
+
+int cdcx_reconstruct_stream(cdcx_ctx* c, const uint8_t* in, size_t len, const int32_t* keys, size_t n_keys,
+                            int32_t** rec8, size_t* n_out) {
+  if (!c || (len && !in) || (n_keys && !keys) || !rec8 || !n_out) return CDCX_ERR_ARG;
+  return guarded(c, [&] {
+    hipStream_t s = c->stream;
+    uint8_t* d = c->buf<uint8_t>("h_file", len);
+    if (len) HIPCHK(hipMemcpyAsync(d, in, len, hipMemcpyHostToDevice, s));
+    int2* dk = c->buf<int2>("h_keys", n_keys);
+    if (n_keys) HIPCHK(hipMemcpyAsync(dk, keys, 8 * n_keys, hipMemcpyHostToDevice, s));
+    decode_batch(c, 1, d, {0}, {(int64_t)len}, dk, (int64_t)n_keys, true, s);
+    std::vector<int32_t> r = c->download(c->d_rec_out, 8 * c->n_rec_out, s);
+    *rec8 = host_copy(r);
+    *n_out = (size_t)c->n_rec_out;
+  });
+}
+
+int cdcx_decode_batch_device(cdcx_ctx* c, int32_t n_ranks, const uint8_t* d_in, const int64_t* in_off,
+                             const int64_t* in_len, const int32_t* d_keys, int64_t n_keys, const int32_t** d_rec_out,
+                             int64_t* n_rec_out, const int32_t** d_perm, void* stream) {
+  if (!c || n_ranks <= 0 || !d_in || !in_off || !in_len || !d_rec_out || !n_rec_out || !d_perm) return CDCX_ERR_ARG;
+  return guarded(c, [&] {
+    std::vector<int64_t> off(in_off, in_off + n_ranks), len(in_len, in_len + n_ranks);
+    decode_batch(c, n_ranks, d_in, off, len, reinterpret_cast<const int2*>(d_keys), n_keys, d_keys != nullptr,
+                 (hipStream_t)stream);
+    *d_rec_out = c->d_rec_out;
+    *n_rec_out = c->n_rec_out;
+    *d_perm = c->d_perm;
+  });
+}
+
+int cdcx_generate_host(const cdcx_gen_params* p, int32_t rank, int32_t** rec8, size_t* n_rec) {
+  if (!p || !rec8 || !n_rec || p->world_size < 2 || p->events_per_rank < 0) return CDCX_ERR_ARG;
+  try {
+    GenArgs g{gen::shape(p->world_size, p->senders, p->sets, p->jitter), 0, p->events_per_rank, p->seed_salt};
+    if (g.sh.T > 16) return CDCX_ERR_LIMIT;
+    std::vector<int32_t> v = generate_host(g, rank);
+    *rec8 = host_copy(v);
+    *n_rec = v.size() / 8;
+    return CDCX_OK;
+  } catch (...) {
+    return CDCX_ERR_NOMEM;
+  }
+}
+
+int cdcx_generate_device(cdcx_ctx* c, const cdcx_gen_params* p, int32_t first_rank, int32_t n_ranks,
+                         const int32_t** d_rec, int64_t* rec_off, void* stream) {
+  if (!c || !p || n_ranks <= 0 || !d_rec || !rec_off || p->world_size < 2 || p->events_per_rank <= 0) return CDCX_ERR_ARG;
+  return guarded(c, [&] {
+    hipStream_t s = (hipStream_t)stream;
+    GenArgs g{gen::shape(p->world_size, p->senders, p->sets, p->jitter), first_rank, p->events_per_rank, p->seed_salt};
+    if (g.sh.T > 16) throw CdcxError{CDCX_ERR_LIMIT, "generator supports at most 16 sets"};
+    const int64_t F = p->events_per_rank;  // frames per rank (upper bound: >= 1 record each)
+    const int32_t tpr = (int32_t)((F + 1023) / 1024);
+    const int64_t NTt = (int64_t)tpr * n_ranks;
+    int32_t* tsr = c->buf<int32_t>("g_tsr", NTt);
+    int32_t* tss = c->buf<int32_t>("g_tss", NTt * 16);
+    int32_t* roff = c->buf<int32_t>("g_roff", F * n_ranks);
+    int32_t* koff = c->buf<int32_t>("g_koff", F * n_ranks);
+    int32_t* nfr = c->buf<int32_t>("g_nfr", n_ranks);
+    int32_t* nmt = c->buf<int32_t>("g_nmt", 16 * n_ranks);
+    int32_t* nrc = c->buf<int32_t>("g_nrc", n_ranks);
+    HIPCHK(hipMemsetAsync(nfr, 0, 4 * n_ranks, s));
+    HIPCHK(hipMemsetAsync(nmt, 0, 64 * n_ranks, s));
+    HIPCHK(hipMemsetAsync(nrc, 0, 4 * n_ranks, s));
+    c->launch(K_GEN_TILE_SUMS, k_gen_tile_sums, dim3(NTt), dim3(256), s, g, F, tpr, tsr, tss);
+    c->launch(K_GEN_RANK_SCAN, k_gen_rank_scan, dim3(n_ranks), dim3(256), s, g, tpr, tsr, tss);
+    c->launch(K_GEN_FRAMES, k_gen_frames, dim3(NTt), dim3(256), s, g, F, tpr, (const int32_t*)tsr, (const int32_t*)tss,
+              roff, koff, nfr, nmt, nrc);
+    std::vector<int32_t> nr = c->download(nrc, n_ranks, s);
+    int64_t* akey = c->buf<int64_t>("g_akey", F * n_ranks);
+    int32_t* inv = c->buf<int32_t>("g_inv", F * n_ranks);
+    c->launch(K_GEN_AKEYS, k_gen_akeys, dim3(blocks(F, 256), n_ranks), dim3(256), s, g, F, (const int32_t*)nmt, akey);
+    c->launch(K_GEN_ARRIVAL, k_gen_arrival, dim3(blocks(F, 256), n_ranks), dim3(256), s, g, F, (const int32_t*)nmt,
+              (const int64_t*)akey, inv);
+    rec_off[0] = 0;
+    for (int r = 0; r < n_ranks; r++) rec_off[r + 1] = rec_off[r] + nr[r];
+    std::vector<int64_t> ro(rec_off, rec_off + n_ranks + 1);
+    int64_t* d_ro = c->upload("g_rec_off", ro, s);
+    int32_t* out = c->buf<int32_t>("g_rec", 8 * rec_off[n_ranks]);
+    c->launch(K_GEN_RECORDS, k_gen_records, dim3(blocks(F, 256), n_ranks), dim3(256), s, g, F, F, (const int32_t*)roff,
+              (const int32_t*)koff, (const int32_t*)nfr, (const int32_t*)nmt, (const int32_t*)inv, (const int64_t*)d_ro,
+              (int4*)out);
+    c->collect(s);
+    c->release("g_akey");
+    c->release("g_inv");
+    c->release("g_roff");
+    c->release("g_koff");
+    *d_rec = out;
+  });
+}
+
+int cdcx_set_profiling(cdcx_ctx* c, int enabled) {
+  if (!c) return CDCX_ERR_ARG;
+  c->profiling = enabled != 0;
+  return CDCX_OK;
+}
+
+int cdcx_kernel_times(cdcx_ctx* c, double* ms, int64_t* launches, int n) {
+  if (!c) return CDCX_ERR_ARG;
+  for (int k = 0; k < n && k < K_COUNT; k++) {
+    if (ms) ms[k] = c->ktime[k];
+    if (launches) launches[k] = c->klaunch[k];
+  }
+  return CDCX_OK;
+}
+
+int cdcx_reset_kernel_times(cdcx_ctx* c) {
+  if (!c) return CDCX_ERR_ARG;
+  std::fill(c->ktime.begin(), c->ktime.end(), 0.0);
+  std::fill(c->klaunch.begin(), c->klaunch.end(), 0);
+  return CDCX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,77 @@
+// cdcx_kernels.h -- declarations of the device kernels (definitions in encode.hip,
+// decode.hip, gen.hip) for the host orchestrator.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "cdcx_layout.h"
+#include "gen.h"
+
+namespace cdcx {
+
+struct GenArgs {
+  gen::Shape sh;
+  int32_t first_rank;
+  int64_t events;
+  uint64_t salt;
+};
+
+// encode.hip
+__global__ void k_set_presence(const int32_t*, const Tile*, uint32_t*, uint32_t*);
+__global__ void k_set_dense(const uint32_t*, int16_t*, int32_t*, int32_t*);
+__global__ void k_tile_hist(const int32_t*, const Tile*, const int16_t*, uint8_t*, uint32_t*);
+__global__ void k_hist_scan(const uint32_t*, const int32_t*, const int32_t*, const int32_t*, const int64_t*, int32_t*,
+                            int32_t*, uint8_t*);
+__global__ void k_scatter(const int32_t*, const Tile*, const uint8_t*, const int32_t*, const int64_t*, TRec*, int32_t*);
+__global__ void k_inc0(const TRec*, const int32_t*, const uint8_t*, const Tile*, const int64_t*, uint8_t*);
+__global__ void k_tile_sum(const uint8_t*, const Tile*, int32_t*);
+__global__ void k_rank_scan(const int32_t*, const int32_t*, const int32_t*, int32_t*);
+__global__ void k_tile_p0(const uint8_t*, const Tile*, const int32_t*, const int64_t*, const int64_t*, int32_t*);
+__global__ void k_chunks(const int32_t*, const int64_t*, const int64_t*, const int32_t*, const uint8_t*, const int32_t*,
+                         const int32_t*, const int32_t*, const int64_t*, int64_t, int2*, int32_t*);
+__global__ void k_units_lb(const Chunk*, int32_t, const int64_t*, const int32_t*, const int32_t*, const int64_t*,
+                           const int32_t*, int2*);
+__global__ void k_unit_prep(Unit*, const TRec*, uint64_t*, int32_t*, int32_t*, int32_t*, uint64_t*, uint32_t*);
+__global__ void k_sort_tiles(const Unit*, const SortTile*, const uint64_t*, uint64_t*, int32_t*, uint64_t*);
+__global__ void k_rank_tiles(const Unit*, const SortTile*, const uint64_t*, const uint64_t*, const int32_t*,
+                             const uint64_t*, int32_t*, int32_t*, uint64_t*);
+__global__ void k_epoch(Unit*, const uint64_t*, uint64_t*, uint64_t*, uint32_t*);
+__global__ void k_chain_lane(Unit*, int32_t, const int32_t*, const int32_t*, int32_t*, int32_t*, int32_t*,
+                             const int64_t*, uint8_t*);
+__global__ void k_positions(const Unit*, const int32_t*, const int32_t*, const uint8_t*, int32_t*, int32_t*, uint32_t*,
+                            int32_t*);
+__global__ void k_deltas(const Unit*, const int32_t*, const uint8_t*, const int32_t*, const int32_t*, const uint32_t*,
+                         const int32_t*, int32_t*, int32_t*);
+__global__ void k_write_units(const Unit*, const int32_t*, const int32_t*, const int32_t*, const uint64_t*,
+                              const uint64_t*, const uint64_t*, const int32_t*, const int32_t*, uint8_t*);
+__global__ void k_chunk_headers(const Chunk*, int32_t, uint8_t*);
+__global__ void k_footer_order(const Unit*, const int32_t*, const int32_t*, const uint64_t*, int32_t, const int64_t*,
+                               const int64_t*, uint64_t*, int32_t*, int32_t*, int32_t*);
+__global__ void k_footer_write(const int64_t*, const int64_t*, const uint64_t*, const int32_t*, const int32_t*,
+                               const int32_t*, const int64_t*, int32_t, uint8_t*);
+__global__ void k_write_keys(const Unit*, const uint64_t*, int2*);
+
+// decode.hip
+__global__ void k_dec_count_chunks(const uint8_t*, const int64_t*, const int64_t*, int32_t, int32_t*, uint32_t*);
+__global__ void k_dec_list_chunks(const uint8_t*, const int64_t*, const int32_t*, const int32_t*, int32_t, DChunk*);
+__global__ void k_dec_units(const uint8_t*, const DChunk*, int32_t, const int32_t*, int32_t*, DUnit*, uint32_t*);
+__global__ void k_dec_sections(const DUnit*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*);
+__global__ void k_dec_perm_lane(const DUnit*, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*, int32_t*,
+                                uint32_t*);
+__global__ void k_dec_records(const DUnit*, const uint8_t*, const int32_t*, const uint64_t*, const uint64_t*,
+                              const int2*, int32_t*, uint8_t*, int4*, uint32_t*);
+
+// gen.hip
+__global__ void k_gen_tile_sums(GenArgs, int64_t, int32_t, int32_t*, int32_t*);
+__global__ void k_gen_rank_scan(GenArgs, int32_t, int32_t*, int32_t*);
+__global__ void k_gen_frames(GenArgs, int64_t, int32_t, const int32_t*, const int32_t*, int32_t*, int32_t*, int32_t*,
+                             int32_t*, int32_t*);
+__global__ void k_gen_akeys(GenArgs, int64_t, const int32_t*, int64_t*);
+__global__ void k_gen_arrival(GenArgs, int64_t, const int32_t*, const int64_t*, int32_t*);
+__global__ void k_gen_records(GenArgs, int64_t, int64_t, const int32_t*, const int32_t*, const int32_t*, const int32_t*,
+                              const int32_t*, const int64_t*, int4*);
+std::vector<int32_t> generate_host(const GenArgs& g, int32_t r);
+
+}  // namespace cdcx

@@ -1,0 +1,89 @@
+// cdcx_layout.h -- descriptors shared by the host orchestrator and the kernels.
+//
+// Vocabulary:
+//   rank   one process's record stream (one rank_<r>.rempi file)
+//   chunk  one extract_encoder_input_format_chunk epoch (<= REMPI_MAX length units)
+//   table  one matching set inside a chunk
+//   unit   (rank, chunk, table): the independent unit of CDC work
+//   T-order  the records of a rank stably partitioned by table (then stream order); every
+//            unit is a contiguous range of it, so per-unit scratch arrays are indexed by the
+//            unit's T-order start `a` without any further allocation.
+#pragma once
+#include <stdint.h>
+
+namespace cdcx {
+
+constexpr int kMaxSets = 256;       // matching_set_id in [0, 256)
+constexpr int kTile = 1024;         // records per tile in record-parallel kernels
+constexpr int kSortTile = 1024;     // matched events per LDS sort tile
+constexpr int kMaxUnitSources = 2048;  // distinct sources per unit held in LDS (epoch)
+
+// Error bits (bit index == CDCX_ERR_* code).
+constexpr uint32_t kErrTruncated = 2, kErrClockOrder = 3, kErrCorrupt = 4, kErrLimit = 6;
+
+struct Tile {
+  int32_t rank;
+  int32_t len;
+  int64_t start;  // global record index
+  int32_t index_in_rank;
+  int32_t pad;
+};
+
+// T-order compact record: {src, clock, index-or-count, info}; info bit31 = matched,
+// bit0 = with_next (matched only).  For unmatched records `x` holds event_count.
+struct TRec {
+  int32_t src;
+  int32_t clk;
+  int32_t x;
+  uint32_t info;
+};
+
+struct Chunk {
+  int32_t rank;
+  int32_t s, e;        // stream positions (inclusive) within the rank
+  int32_t first_unit;  // global unit index
+  int32_t n_units;
+  int32_t pad;
+  int64_t out_off;     // byte offset of the chunk's size_t header in the batch output
+  int64_t payload;     // payload bytes
+};
+
+struct Unit {
+  int64_t a;        // T-order start (global)
+  int32_t n;        // T-order length
+  int32_t rank;
+  int32_t chunk;    // global chunk index
+  int32_t set_id;
+  int32_t M, U, W, S, P;  // matched, unmatched runs, with_next, epoch sources, pairs
+  int32_t K;              // chain length (M - P)
+  int32_t sort_tile0;     // first global sort tile of the unit
+  int64_t out_off;        // byte offset of the unit in the batch output
+  int64_t key_off;        // offset of its sorted keys in the batch key list
+};
+
+// Decoder-side unit: section offsets inside the input buffer.
+struct DUnit {
+  int64_t base;     // byte offset of the unit's first field
+  int32_t rank;
+  int32_t set_id;
+  int32_t M;        // count
+  int32_t S, W, Mi, U, Uc, P;
+  int64_t ep_off, wp_off, mi_off, uid_off, ucnt_off, pair_off;
+  int64_t wbase;    // element offset into decoder scratch (sum of M + 1 over earlier units)
+  int64_t rec_off;  // record offset of the unit's reconstructed stream
+  int64_t key_off;  // offset of its sorted keys
+};
+
+struct SortTile {
+  int32_t unit;
+  int32_t tile;
+};
+
+struct DChunk {
+  int64_t off;  // absolute payload offset in the input buffer
+  int64_t len;
+  int32_t rank;
+  int32_t pad;
+};
+
+}  // namespace cdcx

@@ -1,0 +1,241 @@
+// decode.hip -- CDC replay-side kernels for gfx950.
+//
+//   framing walk (read_record_file :933-978) -> unit section table (decode :1044-1200)
+//   -> inverse linear prediction of with_previous / unmatched ids / ids / delays as two
+//   chained prefix sums (rempi_compression_util.cpp:157-168) -> permutation rebuild
+//   (cdc_prepare_decode_indices :1301-1386) -> per-table observed record stream.
+#include <hip/hip_runtime.h>
+
+#include "cdcx_device.h"
+#include "cdcx_kernels.h"
+
+namespace cdcx {
+
+// One lane per rank file: count chunks, validate the framing and the footer.
+__global__ void __launch_bounds__(64) k_dec_count_chunks(const uint8_t* __restrict__ in, const int64_t* __restrict__ off,
+                                                         const int64_t* __restrict__ len, int32_t n_ranks,
+                                                         int32_t* __restrict__ nchunks, uint32_t* err) {
+  const int r = blockIdx.x * 64 + threadIdx.x;
+  if (r >= n_ranks) return;
+  const uint8_t* b = in + off[r];
+  const int64_t L = len[r];
+  int64_t p = 0;
+  int32_t k = 0;
+  while (true) {
+    if (p + 8 > L) { raise_error(err, kErrCorrupt); break; }
+    const uint64_t n = ld_u64(b + p);
+    p += 8;
+    if (n == 0) {
+      if (p + 8 > L) { raise_error(err, kErrCorrupt); break; }
+      const uint64_t nr = ld_u64(b + p);
+      if (nr > (uint64_t)L || p + 8 + 4 * (int64_t)nr + 4 > L) raise_error(err, kErrCorrupt);
+      break;
+    }
+    if ((n & 7) || n > (uint64_t)(L - p)) { raise_error(err, kErrCorrupt); break; }
+    p += (int64_t)n;
+    k++;
+  }
+  nchunks[r] = k;
+}
+
+__global__ void __launch_bounds__(64) k_dec_list_chunks(const uint8_t* __restrict__ in, const int64_t* __restrict__ off,
+                                                        const int32_t* __restrict__ cbase, const int32_t* __restrict__ nchunks,
+                                                        int32_t n_ranks, DChunk* __restrict__ chunks) {
+  const int r = blockIdx.x * 64 + threadIdx.x;
+  if (r >= n_ranks) return;
+  int64_t p = off[r];
+  for (int32_t k = 0; k < nchunks[r]; k++) {
+    const uint64_t n = ld_u64(in + p);
+    chunks[cbase[r] + k] = DChunk{p + 8, (int64_t)n, r, 0};
+    p += 8 + (int64_t)n;
+  }
+}
+
+// Walk the tables of one chunk payload.  When `units` is null only counts.
+__device__ bool walk_units(const uint8_t* __restrict__ in, const DChunk& c, int32_t first_unit, DUnit* units,
+                           int32_t* count) {
+  int64_t q = c.off;
+  const int64_t end = c.off + c.len;
+  int32_t k = 0;
+  auto need = [&](int64_t bytes) { return q + bytes <= end; };
+  while (q < end) {
+    DUnit u{};
+    u.base = q;
+    u.rank = c.rank;
+    if (!need(16)) return false;
+    u.set_id = (int32_t)ld_u32(in + q);
+    u.M = (int32_t)ld_u32(in + q + 4);
+    const uint64_t esz = ld_u64(in + q + 8);
+    if ((esz & 7) || esz > (uint64_t)(end - q)) return false;
+    u.S = (int32_t)(esz / 8);
+    u.ep_off = q + 16;
+    q += 16 + 2 * (int64_t)esz;
+    if (!need(16)) return false;
+    const uint64_t wsz = ld_u64(in + q + 8);
+    if ((wsz & 7) || wsz > (uint64_t)(end - q)) return false;
+    u.W = (int32_t)(wsz / 8);
+    u.wp_off = q + 16;
+    q += 16 + (int64_t)wsz;
+    if (!need(16)) return false;
+    const uint64_t msz = ld_u64(in + q + 8);
+    if ((msz & 7) || msz > (uint64_t)(end - q)) return false;
+    u.Mi = (int32_t)(msz / 8);
+    u.mi_off = q + 16;
+    q += 16 + (int64_t)msz;
+    if (!need(8)) return false;
+    const uint64_t usz = ld_u64(in + q);
+    if ((usz & 7) || usz > (uint64_t)(end - q)) return false;
+    u.U = (int32_t)(usz / 8);
+    u.uid_off = q + 8;
+    q += 8 + (int64_t)usz;
+    if (!need(8)) return false;
+    const uint64_t csz = ld_u64(in + q);
+    if ((csz & 7) || csz > (uint64_t)(end - q)) return false;
+    u.Uc = (int32_t)(csz / 8);
+    u.ucnt_off = q + 8;
+    q += 8 + (int64_t)csz;
+    if (!need(8)) return false;
+    const uint64_t psz = ld_u64(in + q);
+    if ((psz & 7) || psz > (uint64_t)(end - q)) return false;
+    u.P = (int32_t)(psz / 8);
+    u.pair_off = q + 8;
+    q += 8 + (int64_t)psz;
+    if (q > end) return false;
+    if (u.M < 0 || u.P > u.M || u.W > u.M || (u.Uc > 0 && u.Uc < u.U)) return false;
+    if (units) units[first_unit + k] = u;
+    k++;
+  }
+  *count = k;
+  return q == end;
+}
+
+__global__ void __launch_bounds__(64) k_dec_units(const uint8_t* __restrict__ in, const DChunk* __restrict__ chunks,
+                                                  int32_t n_chunks, const int32_t* __restrict__ first_unit,
+                                                  int32_t* __restrict__ nunits, DUnit* __restrict__ units, uint32_t* err) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= n_chunks) return;
+  int32_t k = 0;
+  if (!walk_units(in, chunks[c], units ? first_unit[c] : 0, units, &k)) raise_error(err, kErrCorrupt);
+  if (nunits) nunits[c] = k;
+}
+
+// Inverse LP of one section: x = prefix(prefix(y)) mod 2^64.  Loads either 8-byte words
+// or sign-extended int32 (the pair sections, rempi_copy_vec_int :1004-1014).
+template <bool I32>
+__device__ void inverse_lp(const uint8_t* __restrict__ src, int32_t n, uint64_t* __restrict__ dst, uint64_t* lds) {
+  uint64_t cz = 0, cx = 0;
+  for (int32_t b = 0; b < n; b += 256) {
+    const int32_t i = b + threadIdx.x;
+    uint64_t y = 0;
+    if (i < n) y = I32 ? sext((int32_t)ld_u32(src + 4 * (int64_t)i)) : ld_u64(src + 8 * (int64_t)i);
+    uint64_t tz, tx;
+    const uint64_t zl = block_exclusive_scan<256>(y, (uint64_t)0, OpAdd(), lds, &tz) + y;
+    const uint64_t z = (i < n) ? zl + cz : 0;
+    const uint64_t xl = block_exclusive_scan<256>(z, (uint64_t)0, OpAdd(), lds, &tx) + z;
+    if (i < n) dst[i] = xl + cx;
+    cx += tx;
+    cz += tz;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_dec_sections(const DUnit* __restrict__ units, const uint8_t* __restrict__ in,
+                                                      uint64_t* __restrict__ wpd, uint64_t* __restrict__ uidd,
+                                                      uint64_t* __restrict__ idd, uint64_t* __restrict__ dld) {
+  __shared__ uint64_t lds[4];
+  const DUnit u = units[blockIdx.x];
+  inverse_lp<false>(in + u.wp_off, u.W, wpd + u.wbase, lds);
+  inverse_lp<false>(in + u.uid_off, u.U, uidd + u.wbase, lds);
+  inverse_lp<true>(in + u.pair_off, u.P, idd + u.wbase, lds);
+  inverse_lp<true>(in + u.pair_off + 4ll * u.P, u.P, dld + u.wbase, lds);
+}
+
+// cdc_prepare_decode_indices, one lane per unit: the list 0..M-1 (+ sentinel M, circular
+// as std::list), each pair moves `id` `delay` nodes past its old successor.
+__global__ void __launch_bounds__(64) k_dec_perm_lane(const DUnit* __restrict__ units, int32_t n_units,
+                                                      const uint64_t* __restrict__ idd, const uint64_t* __restrict__ dld,
+                                                      int32_t* __restrict__ nx, int32_t* __restrict__ pv,
+                                                      int32_t* __restrict__ perm, uint32_t* err) {
+  const int ui = blockIdx.x * 64 + threadIdx.x;
+  if (ui >= n_units) return;
+  const DUnit u = units[ui];
+  const int32_t M = u.M;
+  int32_t* n = nx + u.wbase;
+  int32_t* p = pv + u.wbase;
+  for (int32_t i = 0; i <= M; i++) {
+    n[i] = (i == M) ? 0 : i + 1;
+    p[i] = (i == 0) ? M : i - 1;
+  }
+  for (int32_t k = 0; k < u.P; k++) {
+    const int32_t id = (int32_t)idd[u.wbase + k];
+    int32_t dl = (int32_t)dld[u.wbase + k];
+    if (id < 0 || id >= M || dl > M || dl < -M) {
+      raise_error(err, kErrCorrupt);
+      return;
+    }
+    int32_t at = n[id];
+    n[p[id]] = n[id];
+    p[n[id]] = p[id];
+    for (; dl > 0; dl--) at = n[at];
+    for (; dl < 0; dl++) at = p[at];
+    const int32_t before = p[at];
+    n[before] = id;
+    p[id] = before;
+    n[id] = at;
+    p[at] = id;
+  }
+  int32_t q = n[M];
+  int32_t* pm = perm + u.key_off;
+  for (int32_t i = 0; i < M; i++, q = n[q]) {
+    if (q < 0 || q >= M) { raise_error(err, kErrCorrupt); return; }
+    pm[q] = i;
+  }
+}
+
+// Records reconstruction for one unit (decoded-record definition ii): matched row i is
+// the event of clock order c_i (c = perm^-1) with the replay-supplied sorted key; its
+// with_next comes from with_previous, its index from matched_index; unmatched run k with
+// id `id` sits right before matched row `id`.
+__global__ void __launch_bounds__(256) k_dec_records(const DUnit* __restrict__ units, const uint8_t* __restrict__ in,
+                                                     const int32_t* __restrict__ perm, const uint64_t* __restrict__ wpd,
+                                                     const uint64_t* __restrict__ uidd, const int2* __restrict__ keys,
+                                                     int32_t* __restrict__ cinv, uint8_t* __restrict__ wnf,
+                                                     int4* __restrict__ rec, uint32_t* err) {
+  const DUnit u = units[blockIdx.x];
+  const int32_t M = u.M;
+  const int32_t U = (u.Uc > 0) ? u.U : 0;
+  int32_t* ci = cinv + u.wbase;
+  uint8_t* wf = wnf + u.wbase;
+  for (int32_t v = threadIdx.x; v < M; v += 256) {
+    ci[perm[u.key_off + v]] = v;
+    wf[v] = 0;
+  }
+  __syncthreads();
+  for (int32_t k = threadIdx.x; k < u.W; k += 256) {
+    const uint64_t w = wpd[u.wbase + k];
+    if (w >= (uint64_t)M) raise_error(err, kErrCorrupt);
+    else wf[w] = 1;
+  }
+  const uint64_t* ids = uidd + u.wbase;
+  for (int32_t k = threadIdx.x; k < U; k += 256) {
+    if (ids[k] > (uint64_t)M || (k > 0 && ids[k] <= ids[k - 1])) { raise_error(err, kErrCorrupt); continue; }
+    const int64_t at = u.rec_off + (int64_t)ids[k] + k;
+    const int32_t cnt = (int32_t)ld_u64(in + u.ucnt_off + 8ll * k);
+    rec[2 * at] = make_int4(cnt, 2, 0, 0);
+    rec[2 * at + 1] = make_int4(0, 0, 0, u.set_id);
+  }
+  __syncthreads();
+  for (int32_t i = threadIdx.x; i < M; i += 256) {
+    int32_t lo = 0, hi = U;  // runs with id <= i
+    while (lo < hi) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (ids[mid] <= (uint64_t)i) lo = mid + 1; else hi = mid;
+    }
+    const int64_t at = u.rec_off + i + lo;
+    const int2 k = keys[u.key_off + ci[i]];
+    const int32_t idx = (int32_t)ld_u64(in + u.mi_off + 8ll * i);
+    rec[2 * at] = make_int4(1, 2, 1, k.x);
+    rec[2 * at + 1] = make_int4(wf[i], idx, k.y, u.set_id);
+  }
+}
+
+}  // namespace cdcx

@@ -1,0 +1,866 @@
+// encode.hip -- CDC record-side kernels for gfx950.
+//
+// Pipeline (one batch = many independent rank streams):
+//   set discovery -> stable partition by table (T-order) -> length increments + prefix
+//   -> chunk boundaries (A3) -> units -> per-unit compaction (A3 add) -> tile sort + merge
+//   rank = clock order (A4) -> epoch line in libstdc++ hash order (A4) -> chain (A7)
+//   -> edit-sequence positions + deltas (A8) -> sizes -> serialization with LP (A5, A6, A9,
+//   A11) -> footer (A12).
+// Integer/byte work only: HBM-bound passes are written for coalesced 16-byte accesses,
+// no MFMA.
+#include <hip/hip_runtime.h>
+
+#include "cdcx_device.h"
+#include "cdcx_kernels.h"
+#include "hash_order.h"
+
+namespace cdcx {
+
+// ---------------------------------------------------------------------------------------
+// Set discovery: which matching_set_ids occur in each rank (limit: [0, kMaxSets)).
+__global__ void __launch_bounds__(256) k_set_presence(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
+                                                      uint32_t* __restrict__ presence, uint32_t* err) {
+  __shared__ uint32_t bm[kMaxSets / 32];
+  if (threadIdx.x < kMaxSets / 32) bm[threadIdx.x] = 0;
+  __syncthreads();
+  const Tile t = tiles[blockIdx.x];
+  for (int i = threadIdx.x; i < t.len; i += blockDim.x) {
+    int32_t sid = rec[(t.start + i) * 8 + 7];
+    if ((uint32_t)sid >= (uint32_t)kMaxSets) raise_error(err, kErrLimit);
+    else atomicOr(&bm[sid >> 5], 1u << (sid & 31));
+  }
+  __syncthreads();
+  if (threadIdx.x < kMaxSets / 32 && bm[threadIdx.x]) atomicOr(&presence[t.rank * (kMaxSets / 32) + threadIdx.x], bm[threadIdx.x]);
+}
+
+// Dense table index per (rank, set id): tables are numbered in ascending set id, which is
+// the order test_tables_map (a std::map) emits them in (rempi_encoder_cdc.cpp:785-800).
+__global__ void __launch_bounds__(kMaxSets) k_set_dense(const uint32_t* __restrict__ presence, int16_t* __restrict__ dense,
+                                                        int32_t* __restrict__ setlist, int32_t* __restrict__ nsets) {
+  const int r = blockIdx.x, sid = threadIdx.x;
+  const uint32_t* p = presence + r * (kMaxSets / 32);
+  const int w = sid >> 5, b = sid & 31;
+  int below = __popc(p[w] & ((1u << b) - 1));
+  for (int i = 0; i < w; i++) below += __popc(p[i]);
+  const bool here = (p[w] >> b) & 1;
+  dense[r * kMaxSets + sid] = here ? (int16_t)below : (int16_t)-1;
+  if (here) setlist[r * kMaxSets + below] = sid;
+  if (sid == kMaxSets - 1) nsets[r] = below + (here ? 1 : 0);
+}
+
+// Per-tile table histogram (and the dense table index of every record).
+__global__ void __launch_bounds__(256) k_tile_hist(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
+                                                   const int16_t* __restrict__ dense, uint8_t* __restrict__ tix,
+                                                   uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kMaxSets];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const Tile t = tiles[blockIdx.x];
+  for (int i = threadIdx.x; i < t.len; i += blockDim.x) {
+    int32_t sid = rec[(t.start + i) * 8 + 7];
+    int d = ((uint32_t)sid < (uint32_t)kMaxSets) ? dense[t.rank * kMaxSets + sid] : 0;
+    tix[t.start + i] = (uint8_t)d;
+    atomicAdd(&h[d], 1u);
+  }
+  __syncthreads();
+  hist[(int64_t)blockIdx.x * kMaxSets + threadIdx.x] = h[threadIdx.x];
+}
+
+// Per rank: exclusive scan of the tile histograms in (table, tile) order -> where each
+// tile's records of each table start in T-order; table starts; first-of-table flags.
+__global__ void __launch_bounds__(256) k_hist_scan(const uint32_t* __restrict__ hist, const int32_t* __restrict__ tile0,
+                                                   const int32_t* __restrict__ ntiles, const int32_t* __restrict__ nsets,
+                                                   const int64_t* __restrict__ rec_off, int32_t* __restrict__ base,
+                                                   int32_t* __restrict__ tstart, uint8_t* __restrict__ tfirst) {
+  __shared__ int32_t lds[4];
+  const int r = blockIdx.x;
+  const int T = nsets[r], t0 = tile0[r], nt = ntiles[r];
+  int32_t run = 0;
+  for (int t = 0; t < T; t++) {
+    if (threadIdx.x == 0) {
+      tstart[r * (kMaxSets + 1) + t] = run;
+      tfirst[rec_off[r] + run] = 1;
+    }
+    for (int c = 0; c < nt; c += 256) {
+      int i = c + threadIdx.x;
+      int32_t v = (i < nt) ? (int32_t)hist[(int64_t)(t0 + i) * kMaxSets + t] : 0;
+      int32_t tot;
+      int32_t ex = block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);
+      if (i < nt) base[(int64_t)(t0 + i) * kMaxSets + t] = run + ex;
+      run += tot;
+    }
+  }
+  if (threadIdx.x == 0) tstart[r * (kMaxSets + 1) + T] = run;
+}
+
+// Stable scatter of records into T-order.  Rounds of 256 consecutive records; within a
+// wave, records with the same table find each other with 8 ballots (one per bit of the
+// table index), which keeps the partition stable for any number of tables.
+__global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
+                                                 const uint8_t* __restrict__ tix, const int32_t* __restrict__ base,
+                                                 const int64_t* __restrict__ rec_off, TRec* __restrict__ trec,
+                                                 int32_t* __restrict__ t2s) {
+  constexpr int ROUNDS = kTile / 256;
+  __shared__ int32_t wc[ROUNDS * 4 * kMaxSets];  // [round][wave][table]
+  for (int i = threadIdx.x; i < ROUNDS * 4 * kMaxSets; i += 256) wc[i] = 0;
+  __syncthreads();
+  const Tile t = tiles[blockIdx.x];
+  const int w = wave_id(), l = lane_id();
+  const uint64_t lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+  int my_t[ROUNDS];
+  int my_rank[ROUNDS];
+#pragma unroll
+  for (int j = 0; j < ROUNDS; j++) {
+    const int i = j * 256 + threadIdx.x;
+    const bool valid = i < t.len;
+    const int tb = valid ? tix[t.start + i] : 0;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      uint64_t m = __ballot((tb >> b) & 1);
+      peers &= ((tb >> b) & 1) ? m : ~m;
+    }
+    my_t[j] = tb;
+    my_rank[j] = __popcll(peers & lt_mask);
+    if (valid && __popcll(peers & lt_mask) == 0) wc[(j * 4 + w) * kMaxSets + tb] = __popcll(peers);
+  }
+  __syncthreads();
+  {  // exclusive scan over (round, wave) for each table: thread = table
+    const int tb = threadIdx.x;
+    int32_t run = 0;
+    for (int k = 0; k < ROUNDS * 4; k++) {
+      int32_t v = wc[k * kMaxSets + tb];
+      wc[k * kMaxSets + tb] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  const int64_t rb = rec_off[t.rank];
+  const int32_t spos0 = (int32_t)(t.start - rb);
+#pragma unroll
+  for (int j = 0; j < ROUNDS; j++) {
+    const int i = j * 256 + threadIdx.x;
+    if (i >= t.len) continue;
+    const int tb = my_t[j];
+    const int32_t pos = base[(int64_t)blockIdx.x * kMaxSets + tb] + wc[(j * 4 + w) * kMaxSets + tb] + my_rank[j];
+    const int4* rp = reinterpret_cast<const int4*>(rec + (t.start + i) * 8);
+    const int4 lo = rp[0], hi = rp[1];
+    // lo = {count, type, flag, rank}, hi = {with_next, index, clock, set}
+    TRec o;
+    const bool matched = (lo.z == 1);
+    o.src = lo.w;
+    o.clk = hi.z;
+    o.x = matched ? hi.y : lo.x;
+    o.info = matched ? (0x80000000u | (hi.x != 0 ? 1u : 0u)) : 0u;
+    trec[rb + pos] = o;
+    t2s[rb + pos] = spos0 + i;
+  }
+}
+
+// inc0: length increment of each record if chunks were infinite (add(), :189-212): 1 for a
+// matched event, 1 for an unmatched event that starts a new run of its table, else 0.
+// Scattered back to stream order.
+__global__ void __launch_bounds__(256) k_inc0(const TRec* __restrict__ trec, const int32_t* __restrict__ t2s,
+                                              const uint8_t* __restrict__ tfirst, const Tile* __restrict__ tiles,
+                                              const int64_t* __restrict__ rec_off, uint8_t* __restrict__ inc0s) {
+  const Tile t = tiles[blockIdx.x];
+  const int64_t rb = rec_off[t.rank];
+  for (int i = threadIdx.x; i < t.len; i += blockDim.x) {
+    const int64_t k = t.start + i;
+    const bool m = trec[k].info >> 31;
+    uint8_t inc = 1;
+    if (!m && !tfirst[k] && !(trec[k - 1].info >> 31)) inc = 0;
+    inc0s[rb + t2s[k]] = inc;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_tile_sum(const uint8_t* __restrict__ v, const Tile* __restrict__ tiles,
+                                                  int32_t* __restrict__ tsum) {
+  __shared__ int32_t lds[4];
+  const Tile t = tiles[blockIdx.x];
+  int32_t s = 0;
+  for (int i = threadIdx.x; i < t.len; i += blockDim.x) s += v[t.start + i];
+  s = block_sum<256>(s, lds);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = s;
+}
+
+__global__ void __launch_bounds__(256) k_rank_scan(const int32_t* __restrict__ tsum, const int32_t* __restrict__ tile0,
+                                                   const int32_t* __restrict__ ntiles, int32_t* __restrict__ toff) {
+  __shared__ int32_t lds[4];
+  const int r = blockIdx.x;
+  const int t0 = tile0[r], nt = ntiles[r];
+  int32_t run = 0;
+  for (int c = 0; c < nt; c += 256) {
+    int i = c + threadIdx.x;
+    int32_t v = (i < nt) ? tsum[t0 + i] : 0, tot;
+    int32_t ex = block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);
+    if (i < nt) toff[t0 + i] = run + ex;
+    run += tot;
+  }
+}
+
+// p0[r][i] = sum of inc0 over stream positions < i (n_r + 1 entries per rank).
+__global__ void __launch_bounds__(256) k_tile_p0(const uint8_t* __restrict__ inc0s, const Tile* __restrict__ tiles,
+                                                 const int32_t* __restrict__ toff, const int64_t* __restrict__ rec_off,
+                                                 const int64_t* __restrict__ nrec, int32_t* __restrict__ p0) {
+  __shared__ int32_t lds[4];
+  const Tile t = tiles[blockIdx.x];
+  const int64_t p0b = rec_off[t.rank] + t.rank;
+  const int64_t spos = t.start - rec_off[t.rank];
+  constexpr int PER = kTile / 256;
+  int32_t v[PER], s = 0;
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    int i = threadIdx.x * PER + j;
+    v[j] = (i < t.len) ? inc0s[t.start + i] : 0;
+    s += v[j];
+  }
+  int32_t tot;
+  int32_t ex = block_exclusive_scan<256>(s, 0, OpAdd(), lds, &tot) + toff[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < PER; j++) {
+    int i = threadIdx.x * PER + j;
+    if (i < t.len) p0[p0b + spos + i] = ex;
+    ex += v[j];
+  }
+  if (spos + t.len == nrec[t.rank] && threadIdx.x == 255) p0[p0b + spos + t.len] = ex;
+}
+
+// Chunk boundaries, one wave per rank (extract_encoder_input_format_chunk, :740-778):
+// a chunk starting at s ends at the first e with L(s,e) > REMPI_MAX and with_next(e) == 0,
+// or at the end of the stream.  L(s,e) = p0[e+1]-p0[s] + #tables whose first record in
+// [s,e] is an unmatched run continuation (inc0 == 0; inside the chunk it starts a run).
+__global__ void __launch_bounds__(64) k_chunks(const int32_t* __restrict__ rec, const int64_t* __restrict__ rec_off,
+                                               const int64_t* __restrict__ nrec, const int32_t* __restrict__ p0,
+                                               const uint8_t* __restrict__ inc0s, const int32_t* __restrict__ t2s,
+                                               const int32_t* __restrict__ tstart, const int32_t* __restrict__ nsets,
+                                               const int64_t* __restrict__ ccap_off, int64_t max_len,
+                                               int2* __restrict__ chunks, int32_t* __restrict__ nchunks) {
+  const int r = blockIdx.x, l = lane_id();
+  const int64_t rb = rec_off[r], p0b = rb + r;
+  const int32_t n = (int32_t)nrec[r];
+  const int T = nsets[r];
+  const int32_t* ts = tstart + r * (kMaxSets + 1);
+  int32_t s = 0, k = 0;
+  while (s < n) {
+    int32_t corr[kMaxSets / 64];  // first-in-chunk unmatched continuation positions
+#pragma unroll
+    for (int q = 0; q < kMaxSets / 64; q++) {
+      const int tb = q * 64 + l;
+      corr[q] = INT32_MAX;
+      if (tb < T) {
+        int32_t lo = ts[tb], hi = ts[tb + 1];
+        while (lo < hi) {
+          int32_t mid = (lo + hi) >> 1;
+          if (t2s[rb + mid] < s) lo = mid + 1; else hi = mid;
+        }
+        if (lo < ts[tb + 1]) {
+          int32_t f = t2s[rb + lo];
+          if (inc0s[rb + f] == 0) corr[q] = f;
+        }
+      }
+    }
+    const int32_t p0s = p0[p0b + s];
+    auto L = [&](int32_t e) -> int64_t {
+      int c = 0;
+#pragma unroll
+      for (int q = 0; q < kMaxSets / 64; q++) c += (corr[q] <= e) ? 1 : 0;
+      c = wave_reduce(c, OpAdd());
+      return (int64_t)(p0[p0b + e + 1] - p0s) + c;
+    };
+    int32_t e;
+    if (L(n - 1) <= max_len) {
+      e = n - 1;
+    } else {
+      int32_t lo = s, hi = n - 1;
+      while (lo < hi) {
+        int32_t mid = lo + ((hi - lo) >> 1);
+        if (L(mid) > max_len) hi = mid; else lo = mid + 1;
+      }
+      e = lo;
+      while (e < n - 1 && rec[(rb + e) * 8 + 4] != 0) e++;
+    }
+    if (l == 0) chunks[ccap_off[r] + k] = make_int2(s, e);
+    k++;
+    s = e + 1;
+  }
+  if (l == 0) nchunks[r] = k;
+}
+
+// For every (chunk, table): the table's T-order sub-range that falls inside the chunk.
+__global__ void __launch_bounds__(256) k_units_lb(const Chunk* __restrict__ ch, int32_t n_chunks,
+                                                  const int64_t* __restrict__ lb_off, const int32_t* __restrict__ nsets,
+                                                  const int32_t* __restrict__ tstart, const int64_t* __restrict__ rec_off,
+                                                  const int32_t* __restrict__ t2s, int2* __restrict__ lohi) {
+  const int c = blockIdx.x;
+  if (c >= n_chunks) return;
+  const Chunk C = ch[c];
+  const int T = nsets[C.rank];
+  const int64_t rb = rec_off[C.rank];
+  const int32_t* ts = tstart + C.rank * (kMaxSets + 1);
+  for (int tb = threadIdx.x; tb < T; tb += blockDim.x) {
+    int32_t r0 = ts[tb], r1 = ts[tb + 1];
+    auto lb = [&](int32_t x) {
+      int32_t lo = r0, hi = r1;
+      while (lo < hi) {
+        int32_t mid = (lo + hi) >> 1;
+        if (t2s[rb + mid] < x) lo = mid + 1; else hi = mid;
+      }
+      return lo;
+    };
+    lohi[lb_off[c] + tb] = make_int2(lb(C.s), lb(C.e + 1));
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Per-unit compaction (add(), :178-218): matched keys/indices in observed order, the
+// with_previous list, unmatched runs (merged while no matched event of the table
+// intervenes) -> counts M, U, W.
+__global__ void __launch_bounds__(256) k_unit_prep(Unit* __restrict__ units, const TRec* __restrict__ trec,
+                                                   uint64_t* __restrict__ mkey, int32_t* __restrict__ midx,
+                                                   int32_t* __restrict__ wp, int32_t* __restrict__ run_id,
+                                                   uint64_t* __restrict__ run_cnt, uint32_t* err) {
+  __shared__ int32_t lds[4];
+  Unit& u = units[blockIdx.x];
+  const int64_t a = u.a;
+  const int32_t n = u.n;
+  int32_t cm = 0, cw = 0, cr = 0;
+  for (int32_t b = 0; b < n; b += 256) {
+    const int32_t k = b + threadIdx.x;
+    const bool valid = k < n;
+    TRec r = valid ? trec[a + k] : TRec{0, 0, 0, 0};
+    const bool m = valid && (r.info >> 31);
+    const bool wn = m && (r.info & 1);
+    bool rs = false;
+    if (valid && !m) rs = (k == 0) || (trec[a + k - 1].info >> 31);
+    int32_t tm, tw, tr;
+    const int32_t mo = block_exclusive_scan<256>((int32_t)m, 0, OpAdd(), lds, &tm);
+    const int32_t wo = block_exclusive_scan<256>((int32_t)wn, 0, OpAdd(), lds, &tw);
+    const int32_t ro = block_exclusive_scan<256>((int32_t)rs, 0, OpAdd(), lds, &tr);
+    if (m) {
+      mkey[a + cm + mo] = pack_key(r.clk, r.src);
+      midx[a + cm + mo] = r.x;
+    }
+    if (wn) wp[a + cw + wo] = cm + mo;
+    if (rs) {
+      uint64_t cnt = sext(r.x);
+      for (int32_t j = k + 1; j < n; j++) {
+        TRec q = trec[a + j];
+        if (q.info >> 31) break;
+        cnt += sext(q.x);
+      }
+      run_id[a + cr + ro] = cm + mo;
+      run_cnt[a + cr + ro] = cnt;
+    }
+    cm += tm;
+    cw += tw;
+    cr += tr;
+  }
+  if (threadIdx.x == 0) {
+    u.M = cm;
+    u.U = cr;
+    u.W = cw;
+    // A table must not end inside a with_next group (format(), :229-233).
+    if (cw > 0 && wp[a + cw - 1] == cm - 1) raise_error(err, kErrTruncated);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Clock order (format(), :235-239).  Sort tiles of <= 1024 matched events in LDS by
+// (key, observed index); then every event's global rank = its rank in its own tile + the
+// number of smaller events in the unit's other tiles (tile min/max prune, binary search
+// where ranges overlap).  Near-sorted traces overlap only with neighbour tiles.
+__global__ void __launch_bounds__(256) k_sort_tiles(const Unit* __restrict__ units, const SortTile* __restrict__ st,
+                                                    const uint64_t* __restrict__ mkey, uint64_t* __restrict__ tkey,
+                                                    int32_t* __restrict__ lrank, uint64_t* __restrict__ tminmax) {
+  __shared__ uint64_t key[kSortTile];
+  __shared__ int16_t idx[kSortTile];
+  const SortTile w = st[blockIdx.x];
+  const Unit u = units[w.unit];
+  const int64_t base = u.a + (int64_t)w.tile * kSortTile;
+  const int len = min(kSortTile, u.M - w.tile * kSortTile);
+  for (int j = threadIdx.x; j < kSortTile; j += 256) {
+    key[j] = (j < len) ? mkey[base + j] : ~0ull;
+    idx[j] = (int16_t)j;
+  }
+  __syncthreads();
+  for (int size = 2; size <= kSortTile; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int p = threadIdx.x; p < kSortTile / 2; p += 256) {
+        const int i = 2 * p - (p & (stride - 1));
+        const int j = i + stride;
+        const bool up = ((i & size) == 0);
+        const uint64_t ki = key[i], kj = key[j];
+        const int16_t ii = idx[i], ij = idx[j];
+        const bool gt = (ki > kj) || (ki == kj && ii > ij);
+        if (gt == up) {
+          key[i] = kj;
+          key[j] = ki;
+          idx[i] = ij;
+          idx[j] = ii;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int r = threadIdx.x; r < len; r += 256) {
+    tkey[base + r] = key[r];
+    lrank[base + idx[r]] = r;
+  }
+  if (threadIdx.x == 0) {
+    tminmax[2 * (u.sort_tile0 + w.tile)] = key[0];
+    tminmax[2 * (u.sort_tile0 + w.tile) + 1] = key[len - 1];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_rank_tiles(const Unit* __restrict__ units, const SortTile* __restrict__ st,
+                                                    const uint64_t* __restrict__ mkey, const uint64_t* __restrict__ tkey,
+                                                    const int32_t* __restrict__ lrank, const uint64_t* __restrict__ tminmax,
+                                                    int32_t* __restrict__ cord, int32_t* __restrict__ inv,
+                                                    uint64_t* __restrict__ skey) {
+  const SortTile w = st[blockIdx.x];
+  const Unit u = units[w.unit];
+  const int nt = (u.M + kSortTile - 1) / kSortTile;
+  const uint64_t* mm = tminmax + 2 * (int64_t)u.sort_tile0;  // {min,max} per tile, L1-resident
+  const int len = min(kSortTile, u.M - w.tile * kSortTile);
+  for (int j = threadIdx.x; j < len; j += 256) {
+    const int32_t i = w.tile * kSortTile + j;
+    const uint64_t x = mkey[u.a + i];
+    int32_t rank = lrank[u.a + i];
+    for (int q = 0; q < nt; q++) {
+      if (q == w.tile) continue;
+      const int qlen = min(kSortTile, u.M - q * kSortTile);
+      const uint64_t* tk = tkey + u.a + (int64_t)q * kSortTile;
+      if (q < w.tile) {  // count keys <= x (equal keys from earlier rows come first)
+        if (mm[2 * q + 1] <= x) { rank += qlen; continue; }
+        if (mm[2 * q] > x) continue;
+        int lo = 0, hi = qlen;
+        while (lo < hi) { int mid = (lo + hi) >> 1; if (tk[mid] <= x) lo = mid + 1; else hi = mid; }
+        rank += lo;
+      } else {  // count keys < x
+        if (mm[2 * q + 1] < x) { rank += qlen; continue; }
+        if (mm[2 * q] >= x) continue;
+        int lo = 0, hi = qlen;
+        while (lo < hi) { int mid = (lo + hi) >> 1; if (tk[mid] < x) lo = mid + 1; else hi = mid; }
+        rank += lo;
+      }
+    }
+    cord[u.a + i] = rank;
+    inv[u.a + rank] = i;
+    skey[u.a + rank] = x;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Epoch line (format(), :246-267): per source the last clock in sorted order, listed in
+// the iteration order of the reference's unordered_map<size_t,size_t> fed in sorted
+// order.  Also the clock-order check of :249-256 (equal (clock, source) keys, clock != 0).
+__global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const uint64_t* __restrict__ skey,
+                                               uint64_t* __restrict__ ep_rank, uint64_t* __restrict__ ep_clk,
+                                               uint32_t* err) {
+  constexpr int HCAP = 2 * kMaxUnitSources;
+  __shared__ int32_t hsrc[HCAP];
+  __shared__ int32_t hpos[HCAP];
+  __shared__ int32_t hclk[HCAP];
+  __shared__ int32_t nlist;
+  // After compaction the hash arrays are reused as the sort buffers and emulator storage.
+  Unit& u = units[blockIdx.x];
+  const int64_t a = u.a;
+  const int32_t M = u.M;
+  for (int i = threadIdx.x; i < HCAP; i += 256) {
+    hsrc[i] = INT32_MIN;
+    hpos[i] = INT32_MAX;
+    hclk[i] = INT32_MIN;
+  }
+  if (threadIdx.x == 0) nlist = 0;
+  __syncthreads();
+  for (int32_t r = threadIdx.x; r < M; r += 256) {
+    const uint64_t k = skey[a + r];
+    const int32_t src = key_source(k), clk = key_clock(k);
+    if (r + 1 < M && skey[a + r + 1] == k && clk != 0) raise_error(err, kErrClockOrder);
+    if (src == INT32_MIN) { raise_error(err, kErrLimit); continue; }
+    uint32_t h = ((uint32_t)src * 2654435761u) % HCAP;
+    for (int probe = 0; probe < HCAP; probe++) {
+      int32_t old = atomicCAS(&hsrc[h], INT32_MIN, src);
+      if (old == INT32_MIN || old == src) {
+        atomicMin(&hpos[h], r);
+        atomicMax(&hclk[h], clk);
+        break;
+      }
+      h = (h + 1) % HCAP;
+    }
+  }
+  __syncthreads();
+  // Compact (src, first sorted position, last clock) triples.
+  __shared__ int32_t lpos[kMaxUnitSources];
+  __shared__ int32_t lsrc[kMaxUnitSources];
+  __shared__ int32_t lclk[kMaxUnitSources];
+  for (int i = threadIdx.x; i < HCAP; i += 256) {
+    if (hsrc[i] != INT32_MIN) {
+      int q = atomicAdd(&nlist, 1);
+      if (q < kMaxUnitSources) {
+        lpos[q] = hpos[i];
+        lsrc[q] = hsrc[i];
+        lclk[q] = hclk[i];
+      }
+    }
+  }
+  __syncthreads();
+  const int S = nlist;
+  if (S > kMaxUnitSources) {
+    if (threadIdx.x == 0) { raise_error(err, kErrLimit); u.S = 0; }
+    return;
+  }
+  int P2 = 1;
+  while (P2 < S) P2 <<= 1;
+  for (int i = S + threadIdx.x; i < P2; i += 256) lpos[i] = INT32_MAX;
+  __syncthreads();
+  // Bitonic sort of the triples by first sorted position = unordered_map insertion order.
+  for (int size = 2; size <= P2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int p = threadIdx.x; p < P2 / 2; p += 256) {
+        const int i = 2 * p - (p & (stride - 1));
+        const int j = i + stride;
+        const bool up = ((i & size) == 0);
+        if ((lpos[i] > lpos[j]) == up) {
+          int32_t t0 = lpos[i]; lpos[i] = lpos[j]; lpos[j] = t0;
+          t0 = lsrc[i]; lsrc[i] = lsrc[j]; lsrc[j] = t0;
+          t0 = lclk[i]; lclk[i] = lclk[j]; lclk[j] = t0;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) {
+    uint64_t* hk = reinterpret_cast<uint64_t*>(hsrc);  // HCAP*4 bytes = kMaxUnitSources*8
+    int32_t* hn = hpos;
+    int32_t* hb = hclk;  // bucket array: capacity HCAP >= hash_bucket_capacity(2048)=2357?
+    HashOrder ho;
+    ho.init(hk, hn, hb);
+    for (int q = 0; q < S; q++) ho.insert_new((uint64_t)(int64_t)lsrc[q]);
+    int j = 0;
+    for (int32_t p = ho.head; p != -1; p = ho.next[p], j++) {
+      ep_rank[a + j] = (uint64_t)(int64_t)lsrc[p];
+      ep_clk[a + j] = (uint64_t)(int64_t)lclk[p];
+    }
+    u.S = S;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Chain (rempi_clock_delta_compression.cpp:93-257, :465-551), one lane per unit.
+// Node i = (row i, column c[i]).  See oracle/cdc_oracle.cpp ChainBuilder for the rule.
+// State lives in the unit's scratch: par/lvl at a+i, the leaf list at w1 (n+1 slots).
+__global__ void __launch_bounds__(64) k_chain_lane(Unit* __restrict__ units, int32_t n_units,
+                                                   const int32_t* __restrict__ cord, const int32_t* __restrict__ inv,
+                                                   int32_t* __restrict__ par, int32_t* __restrict__ lvl,
+                                                   int32_t* __restrict__ leaves, const int64_t* __restrict__ w1,
+                                                   uint8_t* __restrict__ chain) {
+  const int ui = blockIdx.x * 64 + threadIdx.x;
+  if (ui >= n_units) return;
+  Unit& u = units[ui];
+  const int64_t a = u.a;
+  const int32_t M = u.M;
+  const int32_t* c = cord + a;
+  const int32_t* iv = inv + a;
+  int32_t* pp = par + a;
+  int32_t* lv = lvl + a;
+  int32_t* lf = leaves + w1[ui];
+  int32_t nl = 0, open = 0;
+  for (int32_t i = 0; i < M; i++) {
+    const int32_t col = c[i];
+    int32_t best_l = 0, best = -1, best_pos = -1;
+    for (int32_t li = 0; li < nl; li++) {
+      const int32_t leaf = lf[li];
+      int32_t s = leaf;
+      while (s >= 0 && c[s] >= col) s = pp[s];
+      if (s >= 0) {
+        const int32_t l = lv[s];
+        if (l > best_l) {
+          best_l = l;
+          best = s;
+          best_pos = (s == leaf) ? li : -1;
+        }
+      }
+    }
+    pp[i] = best;
+    lv[i] = best_l + 1;
+    if (best_pos >= 0) {
+      for (int32_t q = best_pos; q + 1 < nl; q++) lf[q] = lf[q + 1];
+      nl--;
+    }
+    lf[nl++] = i;
+    if (col == open) {
+      int32_t w = 0;
+      for (int32_t q = 0; q < nl; q++)
+        if (c[lf[q]] >= open) lf[w++] = lf[q];
+      nl = w;
+    }
+    while (open < M && iv[open] <= i) open++;
+  }
+  // Final node (M, M): every node is below-left of it, so each leaf is its own candidate.
+  int32_t best_l = 0, best = -1;
+  for (int32_t li = 0; li < nl; li++) {
+    const int32_t l = lv[lf[li]];
+    if (l > best_l) { best_l = l; best = lf[li]; }
+  }
+  int32_t K = 0;
+  for (int32_t s = best; s >= 0; s = pp[s]) {
+    chain[a + s] = 1;
+    K++;
+  }
+  u.K = K;
+  u.P = M - K;
+}
+
+// ---------------------------------------------------------------------------------------
+// Edit-sequence positions (A8).  With chain rows r_1<..<r_K (columns col_k) and r_0 =
+// col_0 = -1, gap k lists ADD(rows r_{k-1}+1..r_k-1), REMOVE(cols col_{k-1}+1..col_k-1),
+// IGNORE(col_k).  Hence, with Kr(r) = #chain rows < r and Kc(j) = #chain cols < j:
+//   ADD of off-chain row r    at r + colprev(r) + 1 - Kr(r)
+//   REMOVE of off-chain col j at rnext(j) + j - Kc(j)
+//   IGNORE of chain row r     at r + c[r] - Kr(r)
+// where colprev = last chain column before row r, rnext = row of the next chain node
+// after column j (M for the end).  seq[2a+pos] = partner position << 2 | type.
+enum : uint32_t { kIgn = 0, kAdd = 1, kRem = 2 };
+
+__global__ void __launch_bounds__(256) k_positions(const Unit* __restrict__ units, const int32_t* __restrict__ cord,
+                                                   const int32_t* __restrict__ inv, const uint8_t* __restrict__ chain,
+                                                   int32_t* __restrict__ posA, int32_t* __restrict__ posR,
+                                                   uint32_t* __restrict__ seq, int32_t* __restrict__ sidx) {
+  __shared__ int32_t lds[4];
+  const Unit u = units[blockIdx.x];
+  const int64_t a = u.a;
+  const int32_t M = u.M;
+  const int32_t* c = cord + a;
+  const int32_t* iv = inv + a;
+  const uint8_t* ch = chain + a;
+  // rows
+  int32_t ck = 0, cc = -1;
+  for (int32_t b = 0; b < M; b += 256) {
+    const int32_t r = b + threadIdx.x;
+    const bool valid = r < M;
+    const bool isc = valid && ch[r];
+    const int32_t cr = valid ? c[r] : -1;
+    int32_t tk, tc;
+    const int32_t kx = block_exclusive_scan<256>((int32_t)isc, 0, OpAdd(), lds, &tk) + ck;
+    int32_t cx = block_exclusive_scan<256>(isc ? cr : -1, -1, OpMax(), lds, &tc);
+    cx = max(cx, cc);
+    if (valid) posA[a + r] = isc ? (r + cr - kx) : (r + cx + 1 - kx);
+    ck += tk;
+    cc = max(cc, tc);
+  }
+  // columns, forward: Kc
+  ck = 0;
+  for (int32_t b = 0; b < M; b += 256) {
+    const int32_t j = b + threadIdx.x;
+    const bool valid = j < M;
+    const bool isc = valid && ch[iv[j]];
+    int32_t tk;
+    const int32_t kx = block_exclusive_scan<256>((int32_t)isc, 0, OpAdd(), lds, &tk) + ck;
+    if (valid) posR[a + j] = -kx;
+    ck += tk;
+  }
+  __syncthreads();
+  // columns, backward: rnext = min chain row among columns > j
+  int32_t cm = M;
+  const int32_t nb = (M + 255) / 256;
+  for (int32_t bb = nb - 1; bb >= 0; bb--) {
+    const int32_t jj = bb * 256 + (255 - threadIdx.x);  // reversed within tile
+    const bool valid = jj < M && jj >= 0;
+    const int32_t row = valid ? iv[jj] : 0;
+    const bool isc = valid && ch[row];
+    int32_t tm;
+    int32_t mx = block_exclusive_scan<256>(isc ? -row : -M, -M, OpMax(), lds, &tm);  // max of -row = -min row
+    int32_t rnext = min(-mx, cm);
+    if (valid) posR[a + jj] = rnext + jj + posR[a + jj];
+    cm = min(cm, -tm);
+  }
+  __syncthreads();
+  // scatter the sequence
+  uint32_t* sq = seq + 2 * a;
+  for (int32_t r = threadIdx.x; r < M; r += 256) {
+    if (ch[r]) {
+      sq[posA[a + r]] = kIgn;
+    } else {
+      const int32_t x = c[r];
+      sq[posA[a + r]] = ((uint32_t)posR[a + x] << 2) | kAdd;
+    }
+  }
+  for (int32_t j = threadIdx.x; j < M; j += 256) {
+    const int32_t row = iv[j];
+    if (!ch[row]) sq[posR[a + j]] = ((uint32_t)posA[a + row] << 2) | kRem;
+  }
+  __syncthreads();
+  // pair index of every second occurrence (pairs are emitted in second-occurrence order)
+  const int32_t L = 2 * u.P + u.K;
+  int32_t carry = 0;
+  for (int32_t b = 0; b < L; b += 256) {
+    const int32_t q = b + threadIdx.x;
+    bool second = false;
+    if (q < L) {
+      const uint32_t e = sq[q];
+      second = (e & 3) != kIgn && (int32_t)(e >> 2) < q;
+    }
+    int32_t t;
+    const int32_t ex = block_exclusive_scan<256>((int32_t)second, 0, OpAdd(), lds, &t);
+    if (second) sidx[2 * a + q] = carry + ex;
+    carry += t;
+  }
+}
+
+// Delta of each off-chain id (convert_to_diff_binary, :358-396): entries strictly
+// between its two occurrences that are in the decoder's list when it moves: IGNOREs,
+// REMOVEs whose element is still pending (its ADD comes later), ADDs whose element has
+// already been moved (its REMOVE came earlier).  Negative when the second occurrence is
+// the REMOVE.
+__global__ void __launch_bounds__(256) k_deltas(const Unit* __restrict__ units, const int32_t* __restrict__ cord,
+                                                const uint8_t* __restrict__ chain, const int32_t* __restrict__ posA,
+                                                const int32_t* __restrict__ posR, const uint32_t* __restrict__ seq,
+                                                const int32_t* __restrict__ sidx, int32_t* __restrict__ pid,
+                                                int32_t* __restrict__ pdl) {
+  const Unit u = units[blockIdx.x];
+  const int64_t a = u.a;
+  const uint32_t* sq = seq + 2 * a;
+  for (int32_t r = threadIdx.x; r < u.M; r += 256) {
+    if (chain[a + r]) continue;
+    const int32_t x = cord[a + r];
+    const int32_t pa = posA[a + r], pr = posR[a + x];
+    const int32_t f = min(pa, pr), s = max(pa, pr);
+    int32_t d = 0;
+    for (int32_t q = f + 1; q < s; q++) {
+      const uint32_t e = sq[q];
+      const uint32_t ty = e & 3;
+      const int32_t pt = (int32_t)(e >> 2);
+      d += (ty == kIgn) | ((ty == kRem) & (pt > s)) | ((ty == kAdd) & (pt < s));
+    }
+    const int32_t k = sidx[2 * a + s];
+    pid[a + k] = x;
+    pdl[a + k] = (pr > pa) ? -d : d;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Serialization of one unit (compress_non_matched_events :627-703,
+// compress_matched_events :706-721, LP of rempi_compression_util.cpp:117-154).
+__device__ __forceinline__ uint64_t lp64(const int32_t* x, int32_t i) {
+  const uint64_t v0 = sext(x[i]);
+  const uint64_t v1 = i >= 1 ? sext(x[i - 1]) : 0;
+  const uint64_t v2 = i >= 2 ? sext(x[i - 2]) : 0;
+  return v0 - 2 * v1 + v2;
+}
+__device__ __forceinline__ uint32_t lp32(const int32_t* x, int32_t i) {
+  const uint32_t v0 = (uint32_t)x[i];
+  const uint32_t v1 = i >= 1 ? (uint32_t)x[i - 1] : 0;
+  const uint32_t v2 = i >= 2 ? (uint32_t)x[i - 2] : 0;
+  return v0 - 2 * v1 + v2;
+}
+
+__global__ void __launch_bounds__(256) k_write_units(const Unit* __restrict__ units, const int32_t* __restrict__ midx,
+                                                     const int32_t* __restrict__ wp, const int32_t* __restrict__ run_id,
+                                                     const uint64_t* __restrict__ run_cnt,
+                                                     const uint64_t* __restrict__ ep_rank,
+                                                     const uint64_t* __restrict__ ep_clk, const int32_t* __restrict__ pid,
+                                                     const int32_t* __restrict__ pdl, uint8_t* __restrict__ out) {
+  const Unit u = units[blockIdx.x];
+  const int64_t a = u.a;
+  uint8_t* o = out + u.out_off;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    st_u32(o, (uint32_t)u.set_id);
+    st_u32(o + 4, (uint32_t)u.M);
+    st_u64(o + 8, 8ull * u.S);
+  }
+  uint8_t* p = o + 16;
+  for (int i = t; i < u.S; i += 256) {
+    st_u64(p + 8 * i, ep_rank[a + i]);
+    st_u64(p + 8 * (u.S + i), ep_clk[a + i]);
+  }
+  p += 16ull * u.S;
+  if (t == 0) {
+    st_u64(p, (uint64_t)u.W);
+    st_u64(p + 8, 8ull * u.W);
+  }
+  p += 16;
+  for (int i = t; i < u.W; i += 256) st_u64(p + 8 * i, lp64(wp + a, i));
+  p += 8ull * u.W;
+  if (t == 0) {
+    st_u64(p, (uint64_t)u.M);
+    st_u64(p + 8, 8ull * u.M);
+  }
+  p += 16;
+  for (int i = t; i < u.M; i += 256) st_u64(p + 8 * i, sext(midx[a + i]));
+  p += 8ull * u.M;
+  if (t == 0) st_u64(p, 8ull * u.U);
+  p += 8;
+  for (int i = t; i < u.U; i += 256) st_u64(p + 8 * i, lp64(run_id + a, i));
+  p += 8ull * u.U;
+  if (t == 0) st_u64(p, 8ull * u.U);
+  p += 8;
+  for (int i = t; i < u.U; i += 256) st_u64(p + 8 * i, run_cnt[a + i]);
+  p += 8ull * u.U;
+  if (t == 0) st_u64(p, 8ull * u.P);
+  p += 8;
+  for (int i = t; i < u.P; i += 256) {
+    st_u32(p + 4 * i, lp32(pid + a, i));
+    st_u32(p + 4ull * u.P + 4 * i, lp32(pdl + a, i));
+  }
+}
+
+__global__ void __launch_bounds__(256) k_chunk_headers(const Chunk* __restrict__ ch, int32_t n, uint8_t* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) st_u64(out + ch[i].out_off, (uint64_t)ch[i].payload);
+}
+
+// Footer (write_footer, :2085-2126): all_epoch_rank_uset (unordered_set<int>) fed with
+// every table's epoch ranks in emitted order; one lane per rank.
+__global__ void __launch_bounds__(64) k_footer_order(const Unit* __restrict__ units, const int32_t* __restrict__ ufirst,
+                                                     const int32_t* __restrict__ nunits, const uint64_t* __restrict__ ep_rank,
+                                                     int32_t n_ranks, const int64_t* __restrict__ fk_off,
+                                                     const int64_t* __restrict__ fb_off, uint64_t* __restrict__ fkey,
+                                                     int32_t* __restrict__ fnext, int32_t* __restrict__ fbucket,
+                                                     int32_t* __restrict__ fcount) {
+  const int r = blockIdx.x * 64 + threadIdx.x;
+  if (r >= n_ranks) return;
+  HashOrder ho;
+  ho.init(fkey + fk_off[r], fnext + fk_off[r], fbucket + fb_off[r]);
+  for (int32_t q = 0; q < nunits[r]; q++) {
+    const Unit u = units[ufirst[r] + q];
+    for (int32_t j = 0; j < u.S; j++) {
+      const uint64_t k = (uint64_t)(int64_t)(int32_t)ep_rank[u.a + j];
+      if (!ho.contains(k)) ho.insert_new(k);
+    }
+  }
+  // Leave the iteration order in fnext's sibling array: rewrite keys in order at fkey.
+  fcount[r] = ho.size;
+  // Store the head so the writer can walk the list.
+  fbucket[fb_off[r]] = ho.head;
+}
+
+__global__ void __launch_bounds__(64) k_footer_write(const int64_t* __restrict__ fk_off, const int64_t* __restrict__ fb_off,
+                                                     const uint64_t* __restrict__ fkey, const int32_t* __restrict__ fnext,
+                                                     const int32_t* __restrict__ fbucket, const int32_t* __restrict__ fcount,
+                                                     const int64_t* __restrict__ foot_off, int32_t n_ranks,
+                                                     uint8_t* __restrict__ out) {
+  const int r = blockIdx.x * 64 + threadIdx.x;
+  if (r >= n_ranks) return;
+  uint8_t* o = out + foot_off[r];
+  st_u64(o, 0);
+  st_u64(o + 8, (uint64_t)fcount[r]);
+  int32_t j = 0;
+  const int64_t kb = fk_off[r];
+  for (int32_t p = fbucket[fb_off[r]]; p != -1; p = fnext[kb + p], j++) st_u32(o + 16 + 4 * j, (uint32_t)fkey[kb + p]);
+  st_u32(o + 16 + 4ull * fcount[r], 0);
+}
+
+// Sorted keys of every unit in file order (the replay side's per-table key stream).
+__global__ void __launch_bounds__(256) k_write_keys(const Unit* __restrict__ units, const uint64_t* __restrict__ skey,
+                                                    int2* __restrict__ keys) {
+  const Unit u = units[blockIdx.x];
+  for (int32_t r = threadIdx.x; r < u.M; r += 256) {
+    const uint64_t k = skey[u.a + r];
+    keys[u.key_off + r] = make_int2(key_source(k), key_clock(k));
+  }
+}
+
+}  // namespace cdcx

@@ -116,3 +116,55 @@ def permutation_stream(c, src: int = 1, set_id: int = 0) -> np.ndarray:
     (observed row i carries clock 10 + c[i] from one source)."""
     recs = [[1, TEST, 1, src, 0, 0, 10 + int(v), set_id] for v in c]
     return np.array(recs, dtype=np.int32).reshape(-1, 8)
+
+
+def chunk_bounds(recs: np.ndarray, max_len: int):
+    """[(start, end_exclusive)] of the chunks extract_encoder_input_format_chunk cuts
+    (rempi_encoder_cdc.cpp:740-778, length rule of add() :178-218)."""
+    recs = np.asarray(recs, dtype=np.int32).reshape(-1, 8)
+    out = []
+    pos, n = 0, recs.shape[0]
+    while pos < n:
+        start, length, last = pos, 0, None
+        last_kind = {}  # set id -> 'm' or 'u' (last record of that table in this chunk)
+        while pos < n:
+            if last is not None and length > max_len and last[4] == 0:
+                break
+            r = recs[pos]
+            s = int(r[7])
+            if r[2] == 1:
+                length += 1
+                last_kind[s] = "m"
+            else:
+                if last_kind.get(s) != "u":
+                    length += 1
+                last_kind[s] = "u"
+            last = r
+            pos += 1
+        out.append((start, pos))
+    return out
+
+
+def expected_table_streams(recs: np.ndarray, max_len: int) -> np.ndarray:
+    """Decoded-record parity target (definition ii): per chunk, per table in
+    ascending set id, the table's records in observed order as the decoder can rebuild them
+    -- consecutive unmatched polls of a table merged (counts summed, add() :205-208),
+    unmatched fields other than count/type/set zeroed, with_next normalised to 0/1, matched
+    event_count 1."""
+    recs = np.asarray(recs, dtype=np.int32).reshape(-1, 8)
+    out = []
+    for a, b in chunk_bounds(recs, max_len):
+        ch = recs[a:b]
+        for s in sorted(set(int(x) for x in ch[:, 7])):
+            prev_unmatched = False
+            for r in ch[ch[:, 7] == s]:
+                if r[2] == 1:
+                    out.append([1, 2, 1, r[3], 1 if r[4] != 0 else 0, r[5], r[6], s])
+                    prev_unmatched = False
+                else:
+                    if prev_unmatched:
+                        out[-1][0] = np.int32(np.int64(out[-1][0]) + np.int64(r[0]))
+                    else:
+                        out.append([r[0], 2, 0, 0, 0, 0, 0, s])
+                    prev_unmatched = True
+    return np.array(out, dtype=np.int32).reshape(-1, 8)

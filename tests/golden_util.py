@@ -1,0 +1,28 @@
+"""Loading the committed golden fixtures (data only, numpy allow_pickle=False)."""
+import glob
+import json
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def names():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return sorted(json.load(f))
+
+
+def load(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    d["max_len"] = int(d["max_len"])
+    d["ref_failed"] = bool(int(d["ref_failed"]))
+    if not d["ref_failed"]:
+        d["rempi"] = d["rempi"].tobytes()
+        d["tables"] = d["tables"].tobytes()
+    return d
+
+
+def all_files():
+    return glob.glob(os.path.join(GOLDEN, "*.npz"))

@@ -1,0 +1,129 @@
+"""HIP path (libcdcx.so) against the reference's bytes/tables (golden fixtures) and the CPU
+oracle on seeded random streams; batch device API against the per-rank oracle.
+All through the C ABI."""
+import numpy as np
+import pytest
+
+import cdc_streams as S
+import golden_util as G
+import oracle_lib as O
+import rempi_amd
+from rempi_amd import cdcx
+
+pytestmark = pytest.mark.gpu
+
+_ctx = {}
+
+
+def ctx(max_len):
+    if max_len not in _ctx:
+        _ctx[max_len] = rempi_amd.Context(max_len)
+    return _ctx[max_len]
+
+
+def first_diff(a: bytes, b: bytes):
+    n = min(len(a), len(b))
+    x = np.frombuffer(a[:n], np.uint8) != np.frombuffer(b[:n], np.uint8)
+    i = int(np.argmax(x)) if x.any() else n
+    return f"len {len(a)} vs {len(b)}, first difference at byte {i}"
+
+
+NAMES = G.names()
+OK_NAMES = [n for n in NAMES if not G.load(n)["ref_failed"]]
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_encode_golden(name):
+    d = G.load(name)
+    c = ctx(d["max_len"])
+    if d["ref_failed"]:
+        with pytest.raises(cdcx.CdcxError) as e:
+            c.encode_stream(d["rec"])
+        assert e.value.code in (2, 3)
+        return
+    got = c.encode_stream(d["rec"])
+    assert got == d["rempi"], first_diff(got, d["rempi"])
+
+
+@pytest.mark.parametrize("name", OK_NAMES)
+def test_decode_golden(name):
+    d = G.load(name)
+    got = ctx(d["max_len"]).decode_stream(d["rempi"])
+    assert got == d["tables"], first_diff(got, d["tables"])
+
+
+@pytest.mark.parametrize("name", OK_NAMES)
+def test_records_golden(name):
+    d = G.load(name)
+    keys = O.sorted_keys(d["rec"], d["max_len"])
+    got = ctx(d["max_len"]).reconstruct_stream(d["rempi"], keys)
+    np.testing.assert_array_equal(got, S.expected_table_streams(d["rec"], d["max_len"]))
+
+
+def test_random_streams_vs_oracle():
+    rng = np.random.default_rng(123)
+    bad = []
+    for t in range(150):
+        mode = ["jitter", "jitter", "sorted", "reversed", "random"][t % 5]
+        recs = S.gen_stream(int(rng.integers(1 << 30)), int(rng.integers(0, 3000)), n_sets=int(rng.integers(1, 5)),
+                            n_senders=int(rng.integers(1, 40)), jitter=int(rng.choice([0, 1, 4, 8, 32])), mode=mode,
+                            p_unmatched=float(rng.choice([0.0, 0.2, 0.7])), p_group=float(rng.choice([0.0, 0.1, 0.5])),
+                            neg_index=bool(t % 4 == 0))
+        mx = int(rng.choice([1, 3, 16, 100, 131072]))
+        try:
+            want, _ = O.encode(recs, mx)
+        except O.OracleError as e:
+            with pytest.raises(cdcx.CdcxError):
+                ctx(mx).encode_stream(recs)
+            continue
+        got = ctx(mx).encode_stream(recs)
+        if got != want:
+            bad.append((t, mode, recs.shape[0], mx, first_diff(got, want)))
+            continue
+        if ctx(mx).decode_stream(want) != O.decode(want):
+            bad.append((t, "decode", recs.shape[0], mx))
+    assert not bad, bad[:5]
+
+
+def test_encode_chunk_payload():
+    rng = np.random.default_rng(5)
+    for t in range(20):
+        recs = S.gen_stream(int(rng.integers(1 << 30)), int(rng.integers(1, 2000)), n_sets=int(rng.integers(1, 5)),
+                            n_senders=int(rng.integers(2, 30)), jitter=8)
+        want, foot = O.encode(recs, 1 << 40)
+        payload, ranks = ctx(131072).encode_chunk(recs)
+        assert payload == want[8:foot]
+        tabs = O.parse_tables(O.decode(want))[0]
+        assert list(ranks) == [int(x) for t_ in tabs for x in t_["epoch_rank"]]
+
+
+@pytest.fixture(scope="module")
+def batch():
+    p = rempi_amd.default_gen_params(world_size=64, events_per_rank=60000)
+    c = ctx(131072)
+    d_rec, rec_off = c.generate_device(p, 5, 4)
+    host = [rempi_amd.generate_host(p, 5 + r) for r in range(4)]
+    return p, c, d_rec, rec_off, host
+
+
+def test_generator_device_matches_host(batch):
+    p, c, d_rec, rec_off, host = batch
+    dev = cdcx.d2h(d_rec, int(rec_off[-1]) * 32, np.int32).reshape(-1, 8)
+    for r in range(4):
+        np.testing.assert_array_equal(dev[rec_off[r]:rec_off[r + 1]], host[r])
+
+
+def test_batch_encode_decode_vs_oracle(batch):
+    p, c, d_rec, rec_off, host = batch
+    d_out, off, ln = c.encode_batch_device(d_rec, rec_off)
+    files = [cdcx.d2h(d_out + int(off[r]), int(ln[r])).tobytes() for r in range(4)]
+    for r in range(4):
+        want, _ = O.encode(host[r], 131072)
+        assert files[r] == want, (r, first_diff(files[r], want))
+    d_keys, n_keys = c.batch_sorted_keys()
+    keys = cdcx.d2h(d_keys, n_keys * 8, np.int32).reshape(-1, 2)
+    np.testing.assert_array_equal(keys, np.concatenate([O.sorted_keys(h, 131072) for h in host]))
+    d_recs, n_recs, d_perm = c.decode_batch_device(d_out, off, ln, d_keys, n_keys)
+    recs = cdcx.d2h(d_recs, n_recs * 32, np.int32).reshape(-1, 8)
+    want = np.concatenate([S.expected_table_streams(h, 131072) for h in host])
+    np.testing.assert_array_equal(recs, want)
