@@ -38,8 +38,14 @@ __global__ void k_sort_tiles(const Unit*, const SortTile*, const uint64_t*, uint
 __global__ void k_rank_tiles(const Unit*, const SortTile*, const uint64_t*, const uint64_t*, const int32_t*,
                              const uint64_t*, int32_t*, int32_t*, uint64_t*);
 __global__ void k_epoch(Unit*, const uint64_t*, uint64_t*, uint64_t*, uint32_t*);
-__global__ void k_chain_lane(Unit*, int32_t, const int32_t*, const int32_t*, int32_t*, int32_t*, int32_t*,
-                             const int64_t*, uint8_t*);
+// chain.hip
+__global__ void k_cuts(Unit*, const int32_t*, int32_t*);
+__global__ void k_seg_list(const Unit*, const int32_t*, Seg*);
+template <int NL>
+__global__ void k_chain_seg(const Unit*, Seg*, int32_t, int32_t*, const int32_t*, const int32_t*, int32_t*, int32_t*,
+                            int32_t*, int32_t*, int32_t*, int32_t*, const int64_t*, uint32_t*);
+__global__ void k_chain_resolve(Unit*, int32_t, const Seg*, const int32_t*, const int32_t*, const int32_t*, uint8_t*,
+                                uint32_t*);
 __global__ void k_positions(const Unit*, const int32_t*, const int32_t*, const uint8_t*, int32_t*, int32_t*, uint32_t*,
                             int32_t*);
 __global__ void k_deltas(const Unit*, const int32_t*, const uint8_t*, const int32_t*, const int32_t*, const uint32_t*,

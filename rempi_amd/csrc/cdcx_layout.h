@@ -57,6 +57,8 @@ struct Unit {
   int32_t M, U, W, S, P;  // matched, unmatched runs, with_next, epoch sources, pairs
   int32_t K;              // chain length (M - P)
   int32_t sort_tile0;     // first global sort tile of the unit
+  int32_t nseg;           // closed-prefix segments of the clock-order permutation
+  int32_t seg0;           // first global segment index
   int64_t out_off;        // byte offset of the unit in the batch output
   int64_t key_off;        // offset of its sorted keys in the batch key list
 };
@@ -72,6 +74,17 @@ struct DUnit {
   int64_t wbase;    // element offset into decoder scratch (sum of M + 1 over earlier units)
   int64_t rec_off;  // record offset of the unit's reconstructed stream
   int64_t key_off;  // offset of its sorted keys
+};
+
+// A closed-prefix segment of one unit's permutation: rows [start, start+len) hold exactly
+// the columns [start, start+len) (max(c[0..start+len-1]) == start+len-1).
+struct Seg {
+  int32_t unit;
+  int32_t ord;    // ordinal within the unit
+  int32_t start;  // first row (= first column)
+  int32_t len;
+  int32_t lmax;   // highest relative level reached (chain levels inside the segment)
+  int32_t qcount; // nodes at lmax
 };
 
 struct SortTile {

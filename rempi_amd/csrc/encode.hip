@@ -548,72 +548,6 @@ __global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const u
 }
 
 // ---------------------------------------------------------------------------------------
-// Chain (rempi_clock_delta_compression.cpp:93-257, :465-551), one lane per unit.
-// Node i = (row i, column c[i]).  See oracle/cdc_oracle.cpp ChainBuilder for the rule.
-// State lives in the unit's scratch: par/lvl at a+i, the leaf list at w1 (n+1 slots).
-__global__ void __launch_bounds__(64) k_chain_lane(Unit* __restrict__ units, int32_t n_units,
-                                                   const int32_t* __restrict__ cord, const int32_t* __restrict__ inv,
-                                                   int32_t* __restrict__ par, int32_t* __restrict__ lvl,
-                                                   int32_t* __restrict__ leaves, const int64_t* __restrict__ w1,
-                                                   uint8_t* __restrict__ chain) {
-  const int ui = blockIdx.x * 64 + threadIdx.x;
-  if (ui >= n_units) return;
-  Unit& u = units[ui];
-  const int64_t a = u.a;
-  const int32_t M = u.M;
-  const int32_t* c = cord + a;
-  const int32_t* iv = inv + a;
-  int32_t* pp = par + a;
-  int32_t* lv = lvl + a;
-  int32_t* lf = leaves + w1[ui];
-  int32_t nl = 0, open = 0;
-  for (int32_t i = 0; i < M; i++) {
-    const int32_t col = c[i];
-    int32_t best_l = 0, best = -1, best_pos = -1;
-    for (int32_t li = 0; li < nl; li++) {
-      const int32_t leaf = lf[li];
-      int32_t s = leaf;
-      while (s >= 0 && c[s] >= col) s = pp[s];
-      if (s >= 0) {
-        const int32_t l = lv[s];
-        if (l > best_l) {
-          best_l = l;
-          best = s;
-          best_pos = (s == leaf) ? li : -1;
-        }
-      }
-    }
-    pp[i] = best;
-    lv[i] = best_l + 1;
-    if (best_pos >= 0) {
-      for (int32_t q = best_pos; q + 1 < nl; q++) lf[q] = lf[q + 1];
-      nl--;
-    }
-    lf[nl++] = i;
-    if (col == open) {
-      int32_t w = 0;
-      for (int32_t q = 0; q < nl; q++)
-        if (c[lf[q]] >= open) lf[w++] = lf[q];
-      nl = w;
-    }
-    while (open < M && iv[open] <= i) open++;
-  }
-  // Final node (M, M): every node is below-left of it, so each leaf is its own candidate.
-  int32_t best_l = 0, best = -1;
-  for (int32_t li = 0; li < nl; li++) {
-    const int32_t l = lv[lf[li]];
-    if (l > best_l) { best_l = l; best = lf[li]; }
-  }
-  int32_t K = 0;
-  for (int32_t s = best; s >= 0; s = pp[s]) {
-    chain[a + s] = 1;
-    K++;
-  }
-  u.K = K;
-  u.P = M - K;
-}
-
-// ---------------------------------------------------------------------------------------
 // Edit-sequence positions (A8).  With chain rows r_1<..<r_K (columns col_k) and r_0 =
 // col_0 = -1, gap k lists ADD(rows r_{k-1}+1..r_k-1), REMOVE(cols col_{k-1}+1..col_k-1),
 // IGNORE(col_k).  Hence, with Kr(r) = #chain rows < r and Kc(j) = #chain cols < j:
