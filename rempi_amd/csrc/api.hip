@@ -24,17 +24,17 @@ namespace {
 
 enum KernelId {
   K_SET_PRESENCE, K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_INC0, K_TILE_SUM, K_RANK_SCAN, K_TILE_P0,
-  K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_CHAIN_SEG, K_CHAIN_RESOLVE, K_POSITIONS, K_DELTAS,
+  K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
   K_WRITE_UNITS, K_CHUNK_HEADERS, K_FOOTER_ORDER, K_FOOTER_WRITE, K_WRITE_KEYS,
-  K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_PERM, K_DEC_RECORDS,
+  K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS,
   K_GEN_TILE_SUMS, K_GEN_RANK_SCAN, K_GEN_FRAMES, K_GEN_AKEYS, K_GEN_ARRIVAL, K_GEN_RECORDS,
   K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
   "k_set_presence", "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_inc0", "k_tile_sum", "k_rank_scan",
-  "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_chain_seg", "k_chain_resolve",
+  "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
-  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_lane", "k_dec_records",
+  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_window1", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
 
 struct HipError {
@@ -89,6 +89,7 @@ struct cdcx_ctx {
   int64_t n_rec_out = 0;
   int32_t* d_perm = nullptr;
   const int32_t* d_gen = nullptr;
+  int32_t last_fallback_units = 0;
 
   template <class T>
   T* buf(const std::string& name, size_t count) {
@@ -394,8 +395,14 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   c->launch(K_CHAIN_SEG, k_chain_seg<16>, dim3((unsigned)std::min<int64_t>(4096, blocks(nsegs, 256))), dim3(256), s,
             (const Unit*)d_units, d_segs, (int32_t)nsegs, d_queue, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par,
             d_lvl, d_exta, d_topg, d_qn, d_leaves, (const int64_t*)d_w1, d_err);
-  c->launch(K_CHAIN_RESOLVE, k_chain_resolve, dim3(blocks(NU, 64)), dim3(64), s, d_units, NU, (const Seg*)d_segs,
-            (const int32_t*)d_par, (const int32_t*)d_exta, (const int32_t*)d_qn, d_chain, d_err);
+  int32_t* d_qexit = c->buf<int32_t>("qexit", N);
+  c->launch(K_CHAIN_EXITS, k_chain_exits, dim3(blocks(nsegs, 256)), dim3(256), s, (const Unit*)d_units,
+            (const Seg*)d_segs, (int32_t)nsegs, (const int32_t*)d_par, (const int32_t*)d_exta, (const int32_t*)d_qn,
+            d_qexit, d_err);
+  c->launch(K_CHAIN_ENTRIES, k_chain_entries, dim3(blocks(NU, 64)), dim3(64), s, d_units, NU, d_segs,
+            (const int32_t*)d_qexit);
+  c->launch(K_CHAIN_MARK, k_chain_mark, dim3(blocks(nsegs, 256)), dim3(256), s, (const Unit*)d_units,
+            (const Seg*)d_segs, (int32_t)nsegs, (const int32_t*)d_par, (const int32_t*)d_qn, d_chain);
   int32_t* d_posA = c->buf<int32_t>("posA", N);
   int32_t* d_posR = c->buf<int32_t>("posR", N);
   uint32_t* d_seq = c->buf<uint32_t>("seq", 2 * N);
@@ -546,9 +553,25 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   int32_t* d_pv = c->buf<int32_t>("d_pv", wb);
   int32_t* d_perm = c->buf<int32_t>("d_perm", ko);
   c->launch(K_DEC_SECTIONS, k_dec_sections, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, d_wpd, d_uidd, d_idd, d_dld);
-  c->launch(K_DEC_PERM, k_dec_perm_lane, dim3(blocks(NU, 64)), dim3(64), s, (const DUnit*)d_units, NU,
-            (const uint64_t*)d_idd, (const uint64_t*)d_dld, d_nx, d_pv, d_perm, d_err);
+  // Permutation rebuild: wave per unit with a 64-slot lane window, then 256 slots, then the
+  // sequential list for whatever is left (decode.hip).
+  int32_t* d_nfail = c->buf<int32_t>("d_nfail", 2);
+  HIPCHK(hipMemsetAsync(d_nfail, 0, 8, s));
+  c->launch(K_DEC_WIN1, k_dec_perm_window<1>, dim3(NU), dim3(64), s, d_units, NU, 0, (const uint64_t*)d_idd,
+            (const uint64_t*)d_dld, d_perm, d_nfail);
+  int32_t nf = c->download(d_nfail, 1, s)[0];
+  if (nf > 0) {
+    c->launch(K_DEC_WIN4, k_dec_perm_window<4>, dim3(NU), dim3(64), s, d_units, NU, 1, (const uint64_t*)d_idd,
+              (const uint64_t*)d_dld, d_perm, d_nfail + 1);
+    nf = c->download(d_nfail + 1, 1, s)[0];
+    if (nf > 0)
+      c->launch(K_DEC_PERM, k_dec_perm_lane, dim3(blocks(NU, 64)), dim3(64), s, (const DUnit*)d_units, NU,
+                (const uint64_t*)d_idd, (const uint64_t*)d_dld, d_nx, d_pv, d_perm, d_err);
+  }
+  c->last_fallback_units = nf;
   c->check_err(d_err, s);
+  units = c->download(d_units, NU, s);
+  c->dunits = units;
   c->d_perm = d_perm;
   c->n_rec_out = ro;
   if (records) {

@@ -44,8 +44,10 @@ __global__ void k_seg_list(const Unit*, const int32_t*, Seg*);
 template <int NL>
 __global__ void k_chain_seg(const Unit*, Seg*, int32_t, int32_t*, const int32_t*, const int32_t*, int32_t*, int32_t*,
                             int32_t*, int32_t*, int32_t*, int32_t*, const int64_t*, uint32_t*);
-__global__ void k_chain_resolve(Unit*, int32_t, const Seg*, const int32_t*, const int32_t*, const int32_t*, uint8_t*,
-                                uint32_t*);
+__global__ void k_chain_exits(const Unit*, const Seg*, int32_t, const int32_t*, const int32_t*, const int32_t*, int32_t*,
+                              uint32_t*);
+__global__ void k_chain_entries(Unit*, int32_t, Seg*, const int32_t*);
+__global__ void k_chain_mark(const Unit*, const Seg*, int32_t, const int32_t*, const int32_t*, uint8_t*);
 __global__ void k_positions(const Unit*, const int32_t*, const int32_t*, const uint8_t*, int32_t*, int32_t*, uint32_t*,
                             int32_t*);
 __global__ void k_deltas(const Unit*, const int32_t*, const uint8_t*, const int32_t*, const int32_t*, const uint32_t*,
@@ -66,6 +68,8 @@ __global__ void k_dec_units(const uint8_t*, const DChunk*, int32_t, const int32_
 __global__ void k_dec_sections(const DUnit*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*);
 __global__ void k_dec_perm_lane(const DUnit*, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*, int32_t*,
                                 uint32_t*);
+template <int K>
+__global__ void k_dec_perm_window(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
 __global__ void k_dec_records(const DUnit*, const uint8_t*, const int32_t*, const uint64_t*, const uint64_t*,
                               const int2*, int32_t*, uint8_t*, int4*, uint32_t*);
 

@@ -74,7 +74,10 @@ struct DUnit {
   int64_t wbase;    // element offset into decoder scratch (sum of M + 1 over earlier units)
   int64_t rec_off;  // record offset of the unit's reconstructed stream
   int64_t key_off;  // offset of its sorted keys
+  int32_t fb;       // permutation rebuild attempt: 0 window K=1, 1 window K=4, 2 sequential
+  int32_t pad2;
 };
+
 
 // A closed-prefix segment of one unit's permutation: rows [start, start+len) hold exactly
 // the columns [start, start+len) (max(c[0..start+len-1]) == start+len-1).
@@ -85,6 +88,8 @@ struct Seg {
   int32_t len;
   int32_t lmax;   // highest relative level reached (chain levels inside the segment)
   int32_t qcount; // nodes at lmax
+  int32_t entry;  // index into the segment's max-level list where the chain enters
+  int32_t pad;
 };
 
 struct SortTile {

@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(256) k_seg_list(const Unit* __restrict__ units
   for (int32_t k = threadIdx.x; k < u.nseg; k += 256) {
     const int32_t e = segend[u.a + k];
     const int32_t s = (k == 0) ? 0 : segend[u.a + k - 1] + 1;
-    segs[u.seg0 + k] = Seg{(int32_t)blockIdx.x, k, s, e - s + 1, 0, 0};
+    segs[u.seg0 + k] = Seg{(int32_t)blockIdx.x, k, s, e - s + 1, 0, 0, 0, 0};
   }
 }
 
@@ -150,24 +150,39 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
     if (ks >= 1) {
       bool found = false;
       if (!slow) {
+        // First slot (creation order) whose level-k* ancestor has a smaller column.  Slots
+        // at level k* are checked in registers; a slot above k* needs a climb through the
+        // parent array, done one slot at a time so the wave's lanes climb together.
+        int32_t cursor = 0;
+        while (true) {
+          int32_t wa = NL, wb = NL;
 #pragma unroll
-        for (int s = 0; s < NL; s++) {
-          if (!found && s < nl && llv[s] >= ks) {
-            int32_t anc;
-            bool ok;
-            if (llv[s] == ks) {
-              anc = lid[s];
-              ok = lcol[s] < c;
-            } else {
-              anc = climb(par, a, lid[s], llv[s] - ks);
-              ok = cord[a + anc] < c;
-            }
-            if (ok) {
-              found = true;
-              pnode = anc;
-              pslot = (llv[s] == ks) ? s : -1;
+          for (int s = NL - 1; s >= 0; s--) {
+            if (s >= cursor && s < nl) {
+              if (llv[s] == ks && lcol[s] < c) wa = s;
+              if (llv[s] > ks) wb = s;
             }
           }
+          if (wa < wb) {
+            found = true;
+            pslot = wa;
+#pragma unroll
+            for (int s = 0; s < NL; s++)
+              if (s == wa) pnode = lid[s];
+            break;
+          }
+          if (wb == NL) break;
+          int32_t L = 0, d = 0;
+#pragma unroll
+          for (int s = 0; s < NL; s++)
+            if (s == wb) { L = lid[s]; d = llv[s] - ks; }
+          const int32_t anc = climb(par, a, L, d);
+          if (cord[a + anc] < c) {
+            found = true;
+            pnode = anc;
+            break;
+          }
+          cursor = wb + 1;
         }
       } else {
         for (int32_t q = 0; q < nl && !found; q++) {
@@ -285,43 +300,71 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
 template __global__ void k_chain_seg<16>(const Unit*, Seg*, int32_t, int32_t*, const int32_t*, const int32_t*, int32_t*,
                                          int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, const int64_t*, uint32_t*);
 
-// Stitch the segments and mark the chain (one lane per unit): start from the earliest
-// max-level node of the last segment; inside a segment follow parents; at a relative-level-1
-// node with ordinal j take Q[j] of the previous segment, or, when j >= |Q|, the parent of
-// its anchor (an earlier relative-level-1 node), repeatedly.
-__global__ void __launch_bounds__(64) k_chain_resolve(Unit* __restrict__ units, int32_t n_units,
-                                                      const Seg* __restrict__ segs, const int32_t* __restrict__ par,
-                                                      const int32_t* __restrict__ exta, const int32_t* __restrict__ qn,
-                                                      uint8_t* __restrict__ chain, uint32_t* err) {
+// Stitching.  From a max-level node of segment s, parents lead down to a relative-level-1
+// node; its outside parent is Q[j] of segment s-1 where j is its ordinal, or, when j >= |Q|,
+// that of its anchor (an earlier relative-level-1 node), repeatedly.
+__device__ __forceinline__ int32_t seg_exit(const int32_t* __restrict__ par, const int32_t* __restrict__ exta,
+                                            int64_t a, int32_t v, int32_t qprev, uint32_t* err) {
+  int32_t p = par[a + v];
+  while (p >= 0) {
+    v = p;
+    p = par[a + v];
+  }
+  int32_t j = -2 - p, guard = 0;
+  while (j >= qprev) {
+    v = exta[a + v];
+    if (v < 0 || ++guard > (1 << 28)) { raise_error(err, kErrCorrupt); return 0; }
+    j = -2 - par[a + v];
+  }
+  return j;
+}
+
+// Where the chain leaves segment s (ord > 0) for each of its max-level nodes.
+__global__ void __launch_bounds__(256) k_chain_exits(const Unit* __restrict__ units, const Seg* __restrict__ segs,
+                                                     int32_t nsegs, const int32_t* __restrict__ par,
+                                                     const int32_t* __restrict__ exta, const int32_t* __restrict__ qn,
+                                                     int32_t* __restrict__ qexit, uint32_t* err) {
+  const int si = blockIdx.x * 256 + threadIdx.x;
+  if (si >= nsegs) return;
+  const Seg sg = segs[si];
+  if (sg.ord == 0) return;
+  const int64_t a = units[sg.unit].a;
+  const int32_t qprev = segs[si - 1].qcount;
+  for (int32_t j = 0; j < sg.qcount; j++) qexit[a + sg.start + j] = seg_exit(par, exta, a, qn[a + sg.start + j], qprev, err);
+}
+
+// Per unit: chain entry index of every segment, last to first; chain length.
+__global__ void __launch_bounds__(64) k_chain_entries(Unit* __restrict__ units, int32_t n_units, Seg* __restrict__ segs,
+                                                      const int32_t* __restrict__ qexit) {
   const int ui = blockIdx.x * 64 + threadIdx.x;
   if (ui >= n_units) return;
   Unit& u = units[ui];
-  const int64_t a = u.a;
-  int32_t K = 0;
-  if (u.M > 0) {
-    int32_t s = u.nseg - 1;
-    int32_t v = qn[a + segs[u.seg0 + s].start];
-    while (true) {
-      chain[a + v] = 1;
-      K++;
-      const int32_t p = par[a + v];
-      if (p >= 0) { v = p; continue; }
-      if (p == -1) break;
-      if (s == 0) { raise_error(err, kErrCorrupt); break; }
-      int32_t j = -2 - p, w = v;
-      const int32_t Q = segs[u.seg0 + s - 1].qcount;
-      int guard = 0;
-      while (j >= Q) {
-        w = exta[a + w];
-        if (w < 0 || ++guard > u.M) { raise_error(err, kErrCorrupt); j = 0; break; }
-        j = -2 - par[a + w];
-      }
-      s--;
-      v = qn[a + segs[u.seg0 + s].start + j];
-    }
+  int32_t j = 0, K = 0;
+  for (int32_t s = u.nseg - 1; s >= 0; s--) {
+    Seg& sg = segs[u.seg0 + s];
+    sg.entry = j;
+    K += sg.lmax;
+    if (s > 0) j = qexit[u.a + sg.start + j];
   }
   u.K = K;
   u.P = u.M - K;
+}
+
+// Mark the chain inside every segment: from its entry node down to relative level 1.
+__global__ void __launch_bounds__(256) k_chain_mark(const Unit* __restrict__ units, const Seg* __restrict__ segs,
+                                                    int32_t nsegs, const int32_t* __restrict__ par,
+                                                    const int32_t* __restrict__ qn, uint8_t* __restrict__ chain) {
+  const int si = blockIdx.x * 256 + threadIdx.x;
+  if (si >= nsegs) return;
+  const Seg sg = segs[si];
+  const int64_t a = units[sg.unit].a;
+  int32_t v = qn[a + sg.start + sg.entry];
+  while (true) {
+    chain[a + v] = 1;
+    const int32_t p = par[a + v];
+    if (p < 0) break;
+    v = p;
+  }
 }
 
 }  // namespace cdcx

@@ -158,6 +158,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_lane(const DUnit* __restrict__ 
   const int ui = blockIdx.x * 64 + threadIdx.x;
   if (ui >= n_units) return;
   const DUnit u = units[ui];
+  if (u.fb != 2) return;  // rebuilt by k_dec_perm_window
   const int32_t M = u.M;
   int32_t* n = nx + u.wbase;
   int32_t* p = pv + u.wbase;
@@ -190,6 +191,192 @@ __global__ void __launch_bounds__(64) k_dec_perm_lane(const DUnit* __restrict__ 
     pm[q] = i;
   }
 }
+
+// ---------------------------------------------------------------------------------------
+// Permutation rebuild, one wave per unit, exact.
+//
+// The list of cdc_prepare_decode_indices is kept as three parts: a settled prefix (already
+// written to perm), a window of W = 64*K slots held across the wave's lanes (slot s in
+// register s/64 of lane s%64), and the untouched suffix nu..M-1 (still the identity).
+// Every pair is uniform across the wave: pull the suffix up to its id, find it (ballots),
+// close the gap (lane shift), step `delay` slots, open a gap and insert (lane shift).  The
+// window's head is settled only when the window is full.  A move that would reach into
+// the settled prefix marks the unit for the next attempt (larger K, then the sequential
+// k_dec_perm_lane); everything written so far is overwritten by that attempt.
+namespace {
+
+template <int K>
+struct Window {
+  int32_t v[K];  // v[j] = slot 64*j + lane
+
+  __device__ __forceinline__ int32_t get(int32_t s) const {  // uniform s
+    int32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < K; j++)
+      if ((s >> 6) == j) r = __shfl(v[j], s & 63, 64);
+    return r;
+  }
+  // position of value x among the first n slots, or -1 (uniform)
+  __device__ __forceinline__ int32_t find(int32_t x, int32_t n) const {
+    const int l = lane_id();
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const uint64_t m = __ballot(v[j] == x && 64 * j + l < n);
+      if (m) return 64 * j + (int32_t)__ffsll((unsigned long long)m) - 1;
+    }
+    return -1;
+  }
+  // slots >= p take the value of slot +1 (p uniform)
+  __device__ __forceinline__ void close_gap(int32_t p) {
+    const int l = lane_id();
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      int32_t nx = __shfl_down(v[j], 1, 64);
+      if (j + 1 < K) {
+        const int32_t wrap = __shfl(v[j + 1], 0, 64);
+        if (l == 63) nx = wrap;
+      }
+      if (64 * j + l >= p) v[j] = nx;
+    }
+  }
+  // slots > t take the value of slot -1, slot t = x
+  __device__ __forceinline__ void open_gap(int32_t t, int32_t x) {
+    const int l = lane_id();
+    int32_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      int32_t pv = __shfl_up(v[j], 1, 64);
+      const int32_t last = __shfl(v[j], 63, 64);
+      if (l == 0) pv = carry;
+      carry = last;
+      const int32_t s = 64 * j + l;
+      if (s > t) v[j] = pv;
+      else if (s == t) v[j] = x;
+    }
+  }
+  // drop the first e slots (e uniform, 0 < e < 64*K)
+  __device__ __forceinline__ void shift_out(int32_t e) {
+    const int l = lane_id();
+    int32_t nv[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const int32_t src = 64 * j + l + e;  // source slot
+      int32_t r = 0;
+#pragma unroll
+      for (int q = 0; q < K; q++) {
+        const int32_t got = __shfl(v[q], src & 63, 64);
+        if ((src >> 6) == q) r = got;
+      }
+      nv[j] = r;
+    }
+#pragma unroll
+    for (int j = 0; j < K; j++) v[j] = nv[j];
+  }
+};
+
+}  // namespace
+
+template <int K>
+__global__ void __launch_bounds__(64) k_dec_perm_window(DUnit* __restrict__ units, int32_t n_units, int32_t want_fb,
+                                                        const uint64_t* __restrict__ idd, const uint64_t* __restrict__ dld,
+                                                        int32_t* __restrict__ perm, int32_t* __restrict__ nfail) {
+  constexpr int32_t W = 64 * K;
+  DUnit& u = units[blockIdx.x];
+  if (u.fb != want_fb) return;
+  const int l = lane_id();
+  const int32_t M = u.M, P = u.P;
+  int32_t* pm = perm + u.key_off;
+  Window<K> win;
+#pragma unroll
+  for (int j = 0; j < K; j++) win.v[j] = -1;
+  int32_t wl = 0, nu = 0, settled = 0;
+  bool fail = false;
+  auto evict = [&](int32_t e) {  // settle the first e slots
+#pragma unroll
+    for (int j = 0; j < K; j++)
+      if (64 * j + l < e) pm[win.v[j]] = settled + 64 * j + l;
+    win.shift_out(e);
+    settled += e;
+    wl -= e;
+  };
+  auto pull = [&](int32_t upto) {  // append suffix elements nu..upto-1 (evicting as needed)
+    while (nu < upto) {
+      int32_t cnt = min(upto - nu, W - wl);
+      if (cnt == 0) {
+        evict(min(wl, W / 2));
+        continue;
+      }
+#pragma unroll
+      for (int j = 0; j < K; j++) {
+        const int32_t s = 64 * j + l;
+        if (s >= wl && s < wl + cnt) win.v[j] = nu + (s - wl);
+      }
+      wl += cnt;
+      nu += cnt;
+    }
+  };
+  for (int32_t k0 = 0; k0 < P && !fail; k0 += 64) {
+    const int32_t idv = (k0 + l < P) ? (int32_t)idd[u.wbase + k0 + l] : 0;
+    const int32_t dlv = (k0 + l < P) ? (int32_t)dld[u.wbase + k0 + l] : 0;
+    const int32_t nk = min(64, P - k0);
+    for (int32_t q = 0; q < nk; q++) {
+      const int32_t x = __shfl(idv, q, 64);
+      const int32_t d = __shfl(dlv, q, 64);
+      if (x < 0 || x >= M) { fail = true; break; }
+      if (x >= nu) pull(x + 1);
+      const int32_t px = win.find(x, wl);
+      if (px < 0) { fail = true; break; }  // already settled
+      win.close_gap(px);
+      wl--;
+      int32_t t = px + d;
+      if (t < 0) { fail = true; break; }
+      while (wl < t) {  // bring the suffix in up to the target slot
+        if (wl == W) {
+          const int32_t e = min(W / 2, t);
+          evict(e);
+          t -= e;
+          continue;
+        }
+        const int32_t cnt = min(t - wl, W - wl);
+        if (nu + cnt > M) { fail = true; break; }
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+          const int32_t s = 64 * j + l;
+          if (s >= wl && s < wl + cnt) win.v[j] = nu + (s - wl);
+        }
+        wl += cnt;
+        nu += cnt;
+      }
+      if (fail) break;
+      if (wl == W) {
+        if (t == 0) {  // x goes right after the settled prefix: settle it directly
+          if (l == 0) pm[x] = settled;
+          settled++;
+          continue;
+        }
+        evict(1);
+        t -= 1;
+      }
+      win.open_gap(t, x);
+      wl++;
+    }
+  }
+  if (fail) {
+    if (l == 0) {
+      u.fb = want_fb + 1;
+      atomicAdd(nfail, 1);
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < K; j++)
+    if (64 * j + l < wl) pm[win.v[j]] = settled + 64 * j + l;
+  settled += wl;
+  for (int32_t v = nu + l; v < M; v += 64) pm[v] = settled + (v - nu);
+}
+
+template __global__ void k_dec_perm_window<1>(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
+template __global__ void k_dec_perm_window<4>(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
 
 // Records reconstruction for one unit (decoded-record definition ii): matched row i is
 // the event of clock order c_i (c = perm^-1) with the replay-supplied sorted key; its

@@ -127,3 +127,19 @@ def test_batch_encode_decode_vs_oracle(batch):
     recs = cdcx.d2h(d_recs, n_recs * 32, np.int32).reshape(-1, 8)
     want = np.concatenate([S.expected_table_streams(h, 131072) for h in host])
     np.testing.assert_array_equal(recs, want)
+
+
+@pytest.mark.parametrize("jitter,world,events,max_len", [(0, 64, 40000, 131072), (32, 256, 120000, 131072),
+                                                          (128, 1024, 60000, 8192), (8, 4, 30000, 512)])
+def test_generator_workloads_vs_oracle(jitter, world, events, max_len):
+    """Synthetic traces across jitter (window/segment fallbacks on the device path)."""
+    p = rempi_amd.default_gen_params(world_size=world, jitter=jitter, events_per_rank=events)
+    c = ctx(max_len)
+    d_rec, rec_off = c.generate_device(p, 1, 2)
+    d_out, off, ln = c.encode_batch_device(d_rec, rec_off)
+    for r in range(2):
+        host = rempi_amd.generate_host(p, 1 + r)
+        want, _ = O.encode(host, max_len)
+        got = cdcx.d2h(d_out + int(off[r]), int(ln[r])).tobytes()
+        assert got == want, (r, first_diff(got, want))
+        assert c.decode_stream(got) == O.decode(want)
