@@ -392,7 +392,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   HIPCHK(hipMemsetAsync(d_queue, 0, 4, s));
   uint8_t* d_chain = c->buf<uint8_t>("chain", N);
   HIPCHK(hipMemsetAsync(d_chain, 0, N, s));
-  c->launch(K_CHAIN_SEG, k_chain_seg<16>, dim3((unsigned)std::min<int64_t>(4096, blocks(nsegs, 256))), dim3(256), s,
+  c->launch(K_CHAIN_SEG, k_chain_seg<16>, dim3((unsigned)std::min<int64_t>(1024, blocks(nsegs, 256))), dim3(256), s,
             (const Unit*)d_units, d_segs, (int32_t)nsegs, d_queue, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par,
             d_lvl, d_exta, d_topg, d_qn, d_leaves, (const int64_t*)d_w1, d_err);
   int32_t* d_qexit = c->buf<int32_t>("qexit", N);

@@ -91,6 +91,13 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
                                                    int32_t* __restrict__ topg, int32_t* __restrict__ qn,
                                                    int32_t* __restrict__ leafg, const int64_t* __restrict__ w1,
                                                    uint32_t* err) {
+  // Work distribution: block b owns the contiguous segments [b*nsegs/B, (b+1)*nsegs/B) and
+  // its lanes take them one at a time from an LDS counter (no global atomics).
+  __shared__ int32_t next_seg;
+  const int32_t seg_lo = (int32_t)((int64_t)blockIdx.x * nsegs / gridDim.x);
+  const int32_t seg_hi = (int32_t)((int64_t)(blockIdx.x + 1) * nsegs / gridDim.x);
+  if (threadIdx.x == 0) next_seg = seg_lo;
+  __syncthreads();
   // lane state
   int32_t si = -1;
   SegCtx S{0, 0, 0, 0, 0};
@@ -109,8 +116,8 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
         segs[si].lmax = lmax;
         segs[si].qcount = qcnt;
       }
-      si = atomicAdd(queue, 1);
-      if (si >= nsegs) break;
+      si = atomicAdd(&next_seg, 1);
+      if (si >= seg_hi) break;
       const Seg sg = segs[si];
       S.a = units[sg.unit].a;
       S.s0 = sg.start;

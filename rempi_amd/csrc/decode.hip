@@ -209,13 +209,6 @@ template <int K>
 struct Window {
   int32_t v[K];  // v[j] = slot 64*j + lane
 
-  __device__ __forceinline__ int32_t get(int32_t s) const {  // uniform s
-    int32_t r = 0;
-#pragma unroll
-    for (int j = 0; j < K; j++)
-      if ((s >> 6) == j) r = __shfl(v[j], s & 63, 64);
-    return r;
-  }
   // position of value x among the first n slots, or -1 (uniform)
   __device__ __forceinline__ int32_t find(int32_t x, int32_t n) const {
     const int l = lane_id();
@@ -231,9 +224,10 @@ struct Window {
     const int l = lane_id();
 #pragma unroll
     for (int j = 0; j < K; j++) {
-      int32_t nx = __shfl_down(v[j], 1, 64);
+      // DPP wave_shl:1 -- lane l reads lane l+1 (no LDS round trip)
+      int32_t nx = __builtin_amdgcn_update_dpp(0, v[j], 0x130, 0xf, 0xf, false);
       if (j + 1 < K) {
-        const int32_t wrap = __shfl(v[j + 1], 0, 64);
+        const int32_t wrap = __builtin_amdgcn_readlane(v[j + 1], 0);
         if (l == 63) nx = wrap;
       }
       if (64 * j + l >= p) v[j] = nx;
@@ -245,8 +239,9 @@ struct Window {
     int32_t carry = 0;
 #pragma unroll
     for (int j = 0; j < K; j++) {
-      int32_t pv = __shfl_up(v[j], 1, 64);
-      const int32_t last = __shfl(v[j], 63, 64);
+      // DPP wave_shr:1 -- lane l reads lane l-1
+      int32_t pv = __builtin_amdgcn_update_dpp(0, v[j], 0x138, 0xf, 0xf, false);
+      const int32_t last = __builtin_amdgcn_readlane(v[j], 63);
       if (l == 0) pv = carry;
       carry = last;
       const int32_t s = 64 * j + l;
@@ -320,8 +315,8 @@ __global__ void __launch_bounds__(64) k_dec_perm_window(DUnit* __restrict__ unit
     const int32_t dlv = (k0 + l < P) ? (int32_t)dld[u.wbase + k0 + l] : 0;
     const int32_t nk = min(64, P - k0);
     for (int32_t q = 0; q < nk; q++) {
-      const int32_t x = __shfl(idv, q, 64);
-      const int32_t d = __shfl(dlv, q, 64);
+      const int32_t x = __builtin_amdgcn_readlane(idv, q);
+      const int32_t d = __builtin_amdgcn_readlane(dlv, q);
       if (x < 0 || x >= M) { fail = true; break; }
       if (x >= nu) pull(x + 1);
       const int32_t px = win.find(x, wl);
