@@ -34,7 +34,7 @@ const char* kKernelNames[K_COUNT] = {
   "k_set_presence", "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_inc0", "k_tile_sum", "k_rank_scan",
   "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
-  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_window1", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records",
+  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_window2", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
 
 struct HipError {
@@ -553,11 +553,11 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   int32_t* d_pv = c->buf<int32_t>("d_pv", wb);
   int32_t* d_perm = c->buf<int32_t>("d_perm", ko);
   c->launch(K_DEC_SECTIONS, k_dec_sections, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, d_wpd, d_uidd, d_idd, d_dld);
-  // Permutation rebuild: wave per unit with a 64-slot lane window, then 256 slots, then the
+  // Permutation rebuild: wave per unit with a 128-slot lane window, then 256 slots, then the
   // sequential list for whatever is left (decode.hip).
   int32_t* d_nfail = c->buf<int32_t>("d_nfail", 2);
   HIPCHK(hipMemsetAsync(d_nfail, 0, 8, s));
-  c->launch(K_DEC_WIN1, k_dec_perm_window<1>, dim3(NU), dim3(64), s, d_units, NU, 0, (const uint64_t*)d_idd,
+  c->launch(K_DEC_WIN1, k_dec_perm_window<2>, dim3(NU), dim3(64), s, d_units, NU, 0, (const uint64_t*)d_idd,
             (const uint64_t*)d_dld, d_perm, d_nfail);
   int32_t nf = c->download(d_nfail, 1, s)[0];
   if (nf > 0) {

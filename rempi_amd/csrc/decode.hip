@@ -370,7 +370,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_window(DUnit* __restrict__ unit
   for (int32_t v = nu + l; v < M; v += 64) pm[v] = settled + (v - nu);
 }
 
-template __global__ void k_dec_perm_window<1>(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
+template __global__ void k_dec_perm_window<2>(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
 template __global__ void k_dec_perm_window<4>(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
 
 // Records reconstruction for one unit (decoded-record definition ii): matched row i is
