@@ -24,7 +24,7 @@ namespace {
 
 enum KernelId {
   K_SET_PRESENCE, K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_INC0, K_TILE_SUM, K_RANK_SCAN, K_TILE_P0,
-  K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
+  K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
   K_WRITE_UNITS, K_CHUNK_HEADERS, K_FOOTER_ORDER, K_FOOTER_WRITE, K_WRITE_KEYS,
   K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS,
   K_GEN_TILE_SUMS, K_GEN_RANK_SCAN, K_GEN_FRAMES, K_GEN_AKEYS, K_GEN_ARRIVAL, K_GEN_RECORDS,
@@ -32,7 +32,7 @@ enum KernelId {
 };
 const char* kKernelNames[K_COUNT] = {
   "k_set_presence", "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_inc0", "k_tile_sum", "k_rank_scan",
-  "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
+  "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
   "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_window2", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
@@ -382,19 +382,23 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   d_units = c->upload("units", units, s);
   Seg* d_segs = c->buf<Seg>("segs", nsegs);
   c->launch(K_SEG_LIST, k_seg_list, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_segend, d_segs);
+  int32_t* d_seghist = c->buf<int32_t>("seghist", 4096);
+  int32_t* d_segord = c->buf<int32_t>("segord", nsegs);
+  HIPCHK(hipMemsetAsync(d_seghist, 0, 4096 * 4, s));
+  c->launch(K_SEG_SORT, k_seg_hist, dim3(blocks(nsegs, 256)), dim3(256), s, (const Seg*)d_segs, (int32_t)nsegs, d_seghist);
+  c->launch(K_SEG_SORT, k_seg_bins, dim3(1), dim3(256), s, d_seghist);
+  c->launch(K_SEG_SORT, k_seg_order, dim3(blocks(nsegs, 256)), dim3(256), s, (const Seg*)d_segs, (int32_t)nsegs, d_seghist,
+            d_segord);
   int32_t* d_par = c->buf<int32_t>("par", N);
-  int32_t* d_lvl = c->buf<int32_t>("lvl", N);
   int32_t* d_exta = c->buf<int32_t>("exta", N);
   int32_t* d_topg = c->buf<int32_t>("topg", N);
   int32_t* d_qn = c->buf<int32_t>("qn", N);
-  int32_t* d_leaves = c->buf<int32_t>("leaves", w1n);
-  int32_t* d_queue = c->buf<int32_t>("queue", 1);
-  HIPCHK(hipMemsetAsync(d_queue, 0, 4, s));
+  int2* d_leaves = c->buf<int2>("leaves", w1n);
   uint8_t* d_chain = c->buf<uint8_t>("chain", N);
   HIPCHK(hipMemsetAsync(d_chain, 0, N, s));
   c->launch(K_CHAIN_SEG, k_chain_seg<16>, dim3((unsigned)std::min<int64_t>(1024, blocks(nsegs, 256))), dim3(256), s,
-            (const Unit*)d_units, d_segs, (int32_t)nsegs, d_queue, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par,
-            d_lvl, d_exta, d_topg, d_qn, d_leaves, (const int64_t*)d_w1, d_err);
+            (const Unit*)d_units, d_segs, (int32_t)nsegs, (const int32_t*)d_segord, (const int32_t*)d_cord,
+            (const int32_t*)d_inv, d_par, d_exta, d_topg, d_qn, d_leaves, (const int64_t*)d_w1, d_err);
   int32_t* d_qexit = c->buf<int32_t>("qexit", N);
   c->launch(K_CHAIN_EXITS, k_chain_exits, dim3(blocks(nsegs, 256)), dim3(256), s, (const Unit*)d_units,
             (const Seg*)d_segs, (int32_t)nsegs, (const int32_t*)d_par, (const int32_t*)d_exta, (const int32_t*)d_qn,

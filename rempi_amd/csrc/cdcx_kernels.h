@@ -41,9 +41,12 @@ __global__ void k_epoch(Unit*, const uint64_t*, uint64_t*, uint64_t*, uint32_t*)
 // chain.hip
 __global__ void k_cuts(Unit*, const int32_t*, int32_t*);
 __global__ void k_seg_list(const Unit*, const int32_t*, Seg*);
+__global__ void k_seg_hist(const Seg*, int32_t, int32_t*);
+__global__ void k_seg_bins(int32_t*);
+__global__ void k_seg_order(const Seg*, int32_t, int32_t*, int32_t*);
 template <int NL>
-__global__ void k_chain_seg(const Unit*, Seg*, int32_t, int32_t*, const int32_t*, const int32_t*, int32_t*, int32_t*,
-                            int32_t*, int32_t*, int32_t*, int32_t*, const int64_t*, uint32_t*);
+__global__ void k_chain_seg(const Unit*, Seg*, int32_t, const int32_t*, const int32_t*, const int32_t*, int32_t*,
+                            int32_t*, int32_t*, int32_t*, int2*, const int64_t*, uint32_t*);
 __global__ void k_chain_exits(const Unit*, const Seg*, int32_t, const int32_t*, const int32_t*, const int32_t*, int32_t*,
                               uint32_t*);
 __global__ void k_chain_entries(Unit*, int32_t, Seg*, const int32_t*);

@@ -65,76 +65,107 @@ __global__ void __launch_bounds__(256) k_seg_list(const Unit* __restrict__ units
   }
 }
 
+// Longest-first order of the segments (counting sort on the length, descending): blocks
+// take strided positions of this order so every block gets a similar amount of work, and a
+// wave's lanes run segments of similar length.
+constexpr int kLenBins = 4096;
+
+__global__ void __launch_bounds__(256) k_seg_hist(const Seg* __restrict__ segs, int32_t nsegs, int32_t* __restrict__ hist) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < nsegs) atomicAdd(&hist[kLenBins - 1 - min(segs[i].len, kLenBins - 1)], 1);
+}
+
+__global__ void __launch_bounds__(256) k_seg_bins(int32_t* __restrict__ hist) {
+  __shared__ int32_t lds[4];
+  int32_t run = 0;
+  for (int b = 0; b < kLenBins; b += 256) {
+    const int32_t v = hist[b + threadIdx.x];
+    int32_t tot;
+    const int32_t ex = block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);
+    hist[b + threadIdx.x] = run + ex;
+    run += tot;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_seg_order(const Seg* __restrict__ segs, int32_t nsegs, int32_t* __restrict__ hist,
+                                                   int32_t* __restrict__ order) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < nsegs) order[atomicAdd(&hist[kLenBins - 1 - min(segs[i].len, kLenBins - 1)], 1)] = i;
+}
+
 namespace {
 
 constexpr int kTopCache = 8;
-
-struct SegCtx {
-  int64_t a;            // unit T-order base (node arrays are indexed a + row)
-  int32_t s0, s1;       // rows [s0, s1)
-  int32_t ord;
-  int64_t lbase;        // global leaf-list base for the slow path
-};
 
 __device__ __forceinline__ int32_t climb(const int32_t* __restrict__ par, int64_t a, int32_t s, int32_t d) {
   for (; d > 0; d--) s = par[a + s];
   return s;
 }
 
+// 4-wide cached reader of one lane's int32 stream (16-byte aligned groups).
+struct Stream4 {
+  int64_t base = -1;
+  int4 v;
+  __device__ __forceinline__ int32_t get(const int32_t* __restrict__ p, int64_t idx) {
+    const int64_t g = idx & ~(int64_t)3;
+    if (g != base) {
+      v = *reinterpret_cast<const int4*>(p + g);
+      base = g;
+    }
+    const int k = (int)(idx & 3);
+    return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+  }
+};
+
 }  // namespace
 
 template <int NL>
 __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ units, Seg* __restrict__ segs, int32_t nsegs,
-                                                   int32_t* __restrict__ queue, const int32_t* __restrict__ cord,
+                                                   const int32_t* __restrict__ order, const int32_t* __restrict__ cord,
                                                    const int32_t* __restrict__ inv, int32_t* __restrict__ par,
-                                                   int32_t* __restrict__ lvl, int32_t* __restrict__ exta,
-                                                   int32_t* __restrict__ topg, int32_t* __restrict__ qn,
-                                                   int32_t* __restrict__ leafg, const int64_t* __restrict__ w1,
-                                                   uint32_t* err) {
-  // Work distribution: block b owns the contiguous segments [b*nsegs/B, (b+1)*nsegs/B) and
-  // its lanes take them one at a time from an LDS counter (no global atomics).
-  __shared__ int32_t next_seg;
-  const int32_t seg_lo = (int32_t)((int64_t)blockIdx.x * nsegs / gridDim.x);
-  const int32_t seg_hi = (int32_t)((int64_t)(blockIdx.x + 1) * nsegs / gridDim.x);
-  if (threadIdx.x == 0) next_seg = seg_lo;
+                                                   int32_t* __restrict__ exta, int32_t* __restrict__ topg,
+                                                   int32_t* __restrict__ qn, int2* __restrict__ leafg,
+                                                   const int64_t* __restrict__ w1, uint32_t* err) {
+  // Block b runs positions b, b+B, b+2B, ... of the longest-first order; its lanes take them
+  // one at a time from an LDS counter.
+  __shared__ int32_t next_j;
+  if (threadIdx.x == 0) next_j = 0;
   __syncthreads();
-  // lane state
   int32_t si = -1;
-  SegCtx S{0, 0, 0, 0, 0};
+  int64_t a = 0, lbase = 0;
+  int32_t s0 = 0, s1 = 0, ord = 0;
   int32_t i = 0, open = 0, nl = 0, lmax = 0, nrel1 = 0, qcnt = 0;
   bool slow = false;
   int32_t lid[NL], llv[NL], lcol[NL];
-  int32_t topR[kTopCache];
+  int32_t topR[kTopCache];  // topR[j] = column of the latest node at level lmax - j
 #pragma unroll
   for (int s = 0; s < NL; s++) lid[s] = llv[s] = lcol[s] = 0;
 #pragma unroll
   for (int j = 0; j < kTopCache; j++) topR[j] = 0;
+  Stream4 cs, is;
 
   while (true) {
-    if (i >= S.s1) {
+    if (i >= s1) {
       if (si >= 0) {
         segs[si].lmax = lmax;
         segs[si].qcount = qcnt;
       }
-      si = atomicAdd(&next_seg, 1);
-      if (si >= seg_hi) break;
+      const int64_t k = (int64_t)blockIdx.x + (int64_t)gridDim.x * atomicAdd(&next_j, 1);
+      if (k >= nsegs) break;
+      si = order[k];
       const Seg sg = segs[si];
-      S.a = units[sg.unit].a;
-      S.s0 = sg.start;
-      S.s1 = sg.start + sg.len;
-      S.ord = sg.ord;
-      S.lbase = w1[sg.unit] + sg.start;
-      i = S.s0;
-      open = S.s0;
-      nl = 0;
-      lmax = 0;
-      nrel1 = 0;
-      qcnt = 0;
+      a = units[sg.unit].a;
+      s0 = sg.start;
+      s1 = sg.start + sg.len;
+      ord = sg.ord;
+      lbase = w1[sg.unit] + sg.start;
+      i = s0;
+      open = s0;
+      nl = lmax = nrel1 = qcnt = 0;
       slow = false;
       continue;
     }
-    const int64_t a = S.a;
-    const int32_t c = cord[a + i];
+    const int32_t c = cs.get(cord, a + i);
 
     // ---- k*: highest level holding a node with a smaller column -----------------------
     int32_t ks = -1;
@@ -143,11 +174,11 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
       if (ks < 0 && j < lmax && topR[j] < c) ks = lmax - j;
     if (ks < 0) {
       ks = 0;
-      if (lmax > kTopCache) {  // binary search levels [1, lmax - kTopCache] of the global tops
-        int32_t lo = 1, hi = lmax - kTopCache;  // largest k in [lo,hi] with top[k] < c
+      if (lmax > kTopCache) {  // binary search the spilled tops of levels [1, lmax - kTopCache]
+        int32_t lo = 1, hi = lmax - kTopCache;
         while (lo <= hi) {
           const int32_t mid = (lo + hi) >> 1;
-          if (topg[a + S.s0 + mid - 1] < c) { ks = mid; lo = mid + 1; } else hi = mid - 1;
+          if (topg[a + s0 + mid - 1] < c) { ks = mid; lo = mid + 1; } else hi = mid - 1;
         }
       }
     }
@@ -157,9 +188,9 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
     if (ks >= 1) {
       bool found = false;
       if (!slow) {
-        // First slot (creation order) whose level-k* ancestor has a smaller column.  Slots
-        // at level k* are checked in registers; a slot above k* needs a climb through the
-        // parent array, done one slot at a time so the wave's lanes climb together.
+        // First slot (creation order) whose level-k* ancestor has a smaller column; slots at
+        // level k* are decided in registers, a slot above k* needs one climb (one at a time,
+        // so the wave's lanes climb together).
         int32_t cursor = 0;
         while (true) {
           int32_t wa = NL, wb = NL;
@@ -193,50 +224,57 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
         }
       } else {
         for (int32_t q = 0; q < nl && !found; q++) {
-          const int32_t L = leafg[S.lbase + q];
-          const int32_t lv = lvl[a + L];
-          if (lv < ks) continue;
-          const int32_t anc = climb(par, a, L, lv - ks);
+          const int2 L = leafg[lbase + q];
+          if (L.y < ks) continue;
+          const int32_t anc = climb(par, a, L.x, L.y - ks);
           if (cord[a + anc] < c) {
             found = true;
             pnode = anc;
-            pslot = (anc == L) ? q : -1;
+            pslot = (anc == L.x) ? q : -1;
           }
         }
       }
       if (!found) raise_error(err, kErrCorrupt);  // cannot happen for a valid permutation
       par[a + i] = pnode;
-    } else if (S.ord == 0) {
+    } else if (ord == 0) {
       par[a + i] = -1;  // first segment: level 1 hangs off the root
     } else {
-      // Outside parent: resolved by k_chain_resolve from (ordinal, first leaf's anchor).
+      // Outside parent: resolved at stitching from (ordinal, anchor of the first leaf).
       par[a + i] = -2 - nrel1;
       int32_t anchor = -1;
       if (nl > 0) {
-        const int32_t L = slow ? leafg[S.lbase] : lid[0];
-        const int32_t lv = slow ? lvl[a + L] : llv[0];
+        int32_t L, lv;
+        if (slow) {
+          const int2 e = leafg[lbase];
+          L = e.x;
+          lv = e.y;
+        } else {
+          L = lid[0];
+          lv = llv[0];
+        }
         anchor = climb(par, a, L, lv - 1);
       }
       exta[a + i] = anchor;
       nrel1++;
     }
 
-    // ---- node, tops, max-level list -----------------------------------------------------
+    // ---- tops (registers; spill only levels that leave the cache) and max-level list ----
     const int32_t k = ks + 1;
-    lvl[a + i] = k;
-    topg[a + S.s0 + ks] = c;
     if (k > lmax) {
+      if (lmax - (kTopCache - 1) >= 1) topg[a + s0 + (lmax - (kTopCache - 1)) - 1] = topR[kTopCache - 1];
 #pragma unroll
       for (int j = kTopCache - 1; j > 0; j--) topR[j] = topR[j - 1];
       topR[0] = c;
       lmax = k;
       qcnt = 0;
-    } else {
+    } else if (lmax - k < kTopCache) {
 #pragma unroll
       for (int j = 0; j < kTopCache; j++)
         if (j == lmax - k) topR[j] = c;
+    } else {
+      topg[a + s0 + k - 1] = c;
     }
-    if (k == lmax) qn[a + S.s0 + qcnt++] = i;
+    if (k == lmax) qn[a + s0 + qcnt++] = i;
 
     // ---- leaf list: drop the adopted leaf, append the new node, sweep ---------------------
     if (!slow) {
@@ -249,11 +287,11 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
             lcol[s] = lcol[s + 1];
           }
         nl--;
-        pslot = -1;  // done; the slow block below must not erase again
+        pslot = -1;
       }
       if (nl == NL) {  // spill and continue exactly on the slow path
 #pragma unroll
-        for (int s = 0; s < NL; s++) leafg[S.lbase + s] = lid[s];
+        for (int s = 0; s < NL; s++) leafg[lbase + s] = make_int2(lid[s], llv[s]);
         slow = true;
       } else {
 #pragma unroll
@@ -268,19 +306,19 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
     }
     if (slow) {
       if (pslot >= 0) {
-        for (int32_t q = pslot; q + 1 < nl; q++) leafg[S.lbase + q] = leafg[S.lbase + q + 1];
+        for (int32_t q = pslot; q + 1 < nl; q++) leafg[lbase + q] = leafg[lbase + q + 1];
         nl--;
       }
-      leafg[S.lbase + nl++] = i;
+      leafg[lbase + nl++] = make_int2(i, k);
     }
     if (c == open) {
       if (!slow) {
-        for (int rep = 0; rep < NL; rep++) {
-          int d = -1;
+        uint32_t dead = 0;
 #pragma unroll
-          for (int s = NL - 1; s >= 0; s--)
-            if (s < nl && lcol[s] < open) d = s;
-          if (d < 0) break;
+        for (int s = 0; s < NL; s++)
+          if (s < nl && lcol[s] < open) dead |= 1u << s;
+        while (dead) {
+          const int d = __ffs(dead) - 1;
 #pragma unroll
           for (int s = 0; s < NL - 1; s++)
             if (s >= d && s + 1 < nl) {
@@ -289,23 +327,25 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
               lcol[s] = lcol[s + 1];
             }
           nl--;
+          dead = (dead & ~(1u << d));
+          dead = (dead & ((1u << d) - 1)) | ((dead >> 1) & ~((1u << d) - 1));
         }
       } else {
         int32_t w = 0;
         for (int32_t q = 0; q < nl; q++) {
-          const int32_t L = leafg[S.lbase + q];
-          if (cord[a + L] >= open) leafg[S.lbase + w++] = L;
+          const int2 L = leafg[lbase + q];
+          if (cord[a + L.x] >= open) leafg[lbase + w++] = L;
         }
         nl = w;
       }
     }
-    while (open < S.s1 && inv[a + open] <= i) open++;
+    while (open < s1 && is.get(inv, a + open) <= i) open++;
     i++;
   }
 }
 
-template __global__ void k_chain_seg<16>(const Unit*, Seg*, int32_t, int32_t*, const int32_t*, const int32_t*, int32_t*,
-                                         int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, const int64_t*, uint32_t*);
+template __global__ void k_chain_seg<16>(const Unit*, Seg*, int32_t, const int32_t*, const int32_t*, const int32_t*,
+                                         int32_t*, int32_t*, int32_t*, int32_t*, int2*, const int64_t*, uint32_t*);
 
 // Stitching.  From a max-level node of segment s, parents lead down to a relative-level-1
 // node; its outside parent is Q[j] of segment s-1 where j is its ordinal, or, when j >= |Q|,
