@@ -152,6 +152,12 @@ int cdcx_set_profiling(cdcx_ctx* ctx, int enabled);
 int cdcx_kernel_times(cdcx_ctx* ctx, double* ms, int64_t* launches, int n);
 int cdcx_reset_kernel_times(cdcx_ctx* ctx);
 
+/* Diagnostics of the chain kernel (enabled by the environment variable CDCX_CHAIN_STATS at
+ * context creation): events, slow-path events, winner-search iterations, climb steps, k*
+ * searches, leaf-list spills, open-column steps, max leaves; copied into out[0..n) and
+ * reset.  Returns CDCX_ERR_ARG when diagnostics are off. */
+int cdcx_chain_stats(cdcx_ctx* ctx, int64_t* out, int n);
+
 #ifdef __cplusplus
 }
 #endif

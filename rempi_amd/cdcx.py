@@ -64,6 +64,7 @@ _SIGNATURES = {
     "cdcx_set_profiling": ([_vp, ctypes.c_int], ctypes.c_int),
     "cdcx_kernel_times": ([_vp, P(ctypes.c_double), _i64p, ctypes.c_int], ctypes.c_int),
     "cdcx_reset_kernel_times": ([_vp], ctypes.c_int),
+    "cdcx_chain_stats": ([_vp, _i64p, ctypes.c_int], ctypes.c_int),
 }
 
 _lib = None
@@ -240,6 +241,13 @@ class Context:
         ln = (ctypes.c_int64 * k)()
         self._check(L.cdcx_kernel_times(self._c, ms, ln, k), "kernel_times")
         return {L.cdcx_kernel_name(i).decode(): (ms[i], ln[i]) for i in range(k)}
+
+    def chain_stats(self):
+        out = np.zeros(8, np.int64)
+        self._check(lib().cdcx_chain_stats(self._c, _ptr(out, ctypes.c_int64), 8), "chain_stats")
+        names = ["events", "slow_events", "winner_iters", "climb_steps", "kstar_searches", "spills", "open_steps",
+                 "max_leaves"]
+        return dict(zip(names, out.tolist()))
 
     def reset_kernel_times(self):
         self._check(lib().cdcx_reset_kernel_times(self._c), "reset_kernel_times")

@@ -90,6 +90,7 @@ struct cdcx_ctx {
   int32_t* d_perm = nullptr;
   const int32_t* d_gen = nullptr;
   int32_t last_fallback_units = 0;
+  bool chain_stats = getenv("CDCX_CHAIN_STATS") != nullptr;
 
   template <class T>
   T* buf(const std::string& name, size_t count) {
@@ -398,7 +399,8 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   HIPCHK(hipMemsetAsync(d_chain, 0, N, s));
   c->launch(K_CHAIN_SEG, k_chain_seg<16>, dim3((unsigned)std::min<int64_t>(1024, blocks(nsegs, 256))), dim3(256), s,
             (const Unit*)d_units, d_segs, (int32_t)nsegs, (const int32_t*)d_segord, (const int32_t*)d_cord,
-            (const int32_t*)d_inv, d_par, d_exta, d_topg, d_qn, d_leaves, (const int64_t*)d_w1, d_err);
+            (const int32_t*)d_inv, d_par, d_exta, d_topg, d_qn, d_leaves, (const int64_t*)d_w1, d_err,
+            c->chain_stats ? c->buf<unsigned long long>("chain_stats", 8) : (unsigned long long*)nullptr);
   int32_t* d_qexit = c->buf<int32_t>("qexit", N);
   c->launch(K_CHAIN_EXITS, k_chain_exits, dim3(blocks(nsegs, 256)), dim3(256), s, (const Unit*)d_units,
             (const Seg*)d_segs, (int32_t)nsegs, (const int32_t*)d_par, (const int32_t*)d_exta, (const int32_t*)d_qn,
@@ -904,6 +906,17 @@ int cdcx_kernel_times(cdcx_ctx* c, double* ms, int64_t* launches, int n) {
     if (launches) launches[k] = c->klaunch[k];
   }
   return CDCX_OK;
+}
+
+int cdcx_chain_stats(cdcx_ctx* c, int64_t* out, int n) {
+  if (!c || !out || !c->chain_stats) return CDCX_ERR_ARG;
+  return guarded(c, [&] {
+    unsigned long long* d = c->buf<unsigned long long>("chain_stats", 8);
+    std::vector<unsigned long long> h = c->download(d, 8, c->stream);
+    for (int k = 0; k < n && k < 8; k++) out[k] = (int64_t)h[k];
+    HIPCHK(hipMemsetAsync(d, 0, 64, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  });
 }
 
 int cdcx_reset_kernel_times(cdcx_ctx* c) {

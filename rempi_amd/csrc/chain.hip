@@ -125,7 +125,12 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
                                                    const int32_t* __restrict__ inv, int32_t* __restrict__ par,
                                                    int32_t* __restrict__ exta, int32_t* __restrict__ topg,
                                                    int32_t* __restrict__ qn, int2* __restrict__ leafg,
-                                                   const int64_t* __restrict__ w1, uint32_t* err) {
+                                                   const int64_t* __restrict__ w1, uint32_t* err,
+                                                   unsigned long long* __restrict__ stats) {
+  // stats (diagnostics, normally null): events, slow events, winner iterations, climb
+  // steps, k* searches, spills, open-advance steps, max leaves
+  unsigned long long st_ev = 0, st_slow = 0, st_win = 0, st_climb = 0, st_ks = 0, st_spill = 0, st_open = 0;
+  int32_t st_maxnl = 0;
   // Block b runs positions b, b+B, b+2B, ... of the longest-first order; its lanes take them
   // one at a time from an LDS counter.
   __shared__ int32_t next_j;
@@ -151,7 +156,19 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
         segs[si].qcount = qcnt;
       }
       const int64_t k = (int64_t)blockIdx.x + (int64_t)gridDim.x * atomicAdd(&next_j, 1);
-      if (k >= nsegs) break;
+      if (k >= nsegs) {
+        if (stats) {
+          atomicAdd(&stats[0], st_ev);
+          atomicAdd(&stats[1], st_slow);
+          atomicAdd(&stats[2], st_win);
+          atomicAdd(&stats[3], st_climb);
+          atomicAdd(&stats[4], st_ks);
+          atomicAdd(&stats[5], st_spill);
+          atomicAdd(&stats[6], st_open);
+          atomicMax(&stats[7], (unsigned long long)st_maxnl);
+        }
+        break;
+      }
       si = order[k];
       const Seg sg = segs[si];
       a = units[sg.unit].a;
@@ -166,6 +183,11 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
       continue;
     }
     const int32_t c = cs.get(cord, a + i);
+    if (stats) {
+      st_ev++;
+      st_slow += slow;
+      st_maxnl = max(st_maxnl, nl);
+    }
 
     // ---- k*: highest level holding a node with a smaller column -----------------------
     int32_t ks = -1;
@@ -174,6 +196,7 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
       if (ks < 0 && j < lmax && topR[j] < c) ks = lmax - j;
     if (ks < 0) {
       ks = 0;
+      if (stats && lmax > kTopCache) st_ks++;
       if (lmax > kTopCache) {  // binary search the spilled tops of levels [1, lmax - kTopCache]
         int32_t lo = 1, hi = lmax - kTopCache;
         while (lo <= hi) {
@@ -193,6 +216,7 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
         // so the wave's lanes climb together).
         int32_t cursor = 0;
         while (true) {
+          if (stats) st_win++;
           int32_t wa = NL, wb = NL;
 #pragma unroll
           for (int s = NL - 1; s >= 0; s--) {
@@ -214,6 +238,7 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
 #pragma unroll
           for (int s = 0; s < NL; s++)
             if (s == wb) { L = lid[s]; d = llv[s] - ks; }
+          if (stats) st_climb += d;
           const int32_t anc = climb(par, a, L, d);
           if (cord[a + anc] < c) {
             found = true;
@@ -293,6 +318,7 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
 #pragma unroll
         for (int s = 0; s < NL; s++) leafg[lbase + s] = make_int2(lid[s], llv[s]);
         slow = true;
+        if (stats) st_spill++;
       } else {
 #pragma unroll
         for (int s = 0; s < NL; s++)
@@ -339,13 +365,17 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
         nl = w;
       }
     }
-    while (open < s1 && is.get(inv, a + open) <= i) open++;
+    while (open < s1 && is.get(inv, a + open) <= i) {
+      open++;
+      if (stats) st_open++;
+    }
     i++;
   }
 }
 
 template __global__ void k_chain_seg<16>(const Unit*, Seg*, int32_t, const int32_t*, const int32_t*, const int32_t*,
-                                         int32_t*, int32_t*, int32_t*, int32_t*, int2*, const int64_t*, uint32_t*);
+                                         int32_t*, int32_t*, int32_t*, int32_t*, int2*, const int64_t*, uint32_t*,
+                                         unsigned long long*);
 
 // Stitching.  From a max-level node of segment s, parents lead down to a relative-level-1
 // node; its outside parent is Q[j] of segment s-1 where j is its ordinal, or, when j >= |Q|,
