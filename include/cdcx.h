@@ -158,6 +158,11 @@ int cdcx_reset_kernel_times(cdcx_ctx* ctx);
  * reset.  Returns CDCX_ERR_ARG when diagnostics are off. */
 int cdcx_chain_stats(cdcx_ctx* ctx, int64_t* out, int n);
 
+/* Segments that entered each chain tier in the last device encode: out[0] all segments
+ * (16-lane groups), out[1] segments whose leaf list outgrew 16 slots (64-lane groups),
+ * out[2] segments that outgrew 64 slots (lane kernel, global-memory leaf list). */
+int cdcx_chain_tiers(cdcx_ctx* ctx, int64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

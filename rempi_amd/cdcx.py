@@ -65,6 +65,7 @@ _SIGNATURES = {
     "cdcx_kernel_times": ([_vp, P(ctypes.c_double), _i64p, ctypes.c_int], ctypes.c_int),
     "cdcx_reset_kernel_times": ([_vp], ctypes.c_int),
     "cdcx_chain_stats": ([_vp, _i64p, ctypes.c_int], ctypes.c_int),
+    "cdcx_chain_tiers": ([_vp, _i64p], ctypes.c_int),
 }
 
 _lib = None
@@ -241,6 +242,12 @@ class Context:
         ln = (ctypes.c_int64 * k)()
         self._check(L.cdcx_kernel_times(self._c, ms, ln, k), "kernel_times")
         return {L.cdcx_kernel_name(i).decode(): (ms[i], ln[i]) for i in range(k)}
+
+    def chain_tiers(self):
+        """Segments entering each chain tier (16-lane, 64-lane, lane kernel) in the last encode."""
+        out = np.zeros(3, dtype=np.int64)
+        self._check(lib().cdcx_chain_tiers(self._c, _ptr(out, ctypes.c_int64)), "chain_tiers")
+        return [int(x) for x in out]
 
     def chain_stats(self):
         out = np.zeros(8, np.int64)

@@ -24,7 +24,7 @@ namespace {
 
 enum KernelId {
   K_SET_PRESENCE, K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_INC0, K_TILE_SUM, K_RANK_SCAN, K_TILE_P0,
-  K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
+  K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_G16, K_CHAIN_G64, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
   K_WRITE_UNITS, K_CHUNK_HEADERS, K_FOOTER_ORDER, K_FOOTER_WRITE, K_WRITE_KEYS,
   K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS,
   K_GEN_TILE_SUMS, K_GEN_RANK_SCAN, K_GEN_FRAMES, K_GEN_AKEYS, K_GEN_ARRIVAL, K_GEN_RECORDS,
@@ -32,7 +32,7 @@ enum KernelId {
 };
 const char* kKernelNames[K_COUNT] = {
   "k_set_presence", "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_inc0", "k_tile_sum", "k_rank_scan",
-  "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
+  "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
   "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_window2", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
@@ -91,6 +91,9 @@ struct cdcx_ctx {
   const int32_t* d_gen = nullptr;
   int32_t last_fallback_units = 0;
   bool chain_stats = getenv("CDCX_CHAIN_STATS") != nullptr;
+  // First chain tier (diagnostics / tests): 0 = 16-lane groups, 1 = 64-lane groups, 2 = lane kernel.
+  int chain_tier = getenv("CDCX_CHAIN_TIER") ? atoi(getenv("CDCX_CHAIN_TIER")) : 0;
+  int64_t chain_tier_counts[3] = {0, 0, 0};  // segments entering each tier in the last encode
 
   template <class T>
   T* buf(const std::string& name, size_t count) {
@@ -397,10 +400,41 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int2* d_leaves = c->buf<int2>("leaves", w1n);
   uint8_t* d_chain = c->buf<uint8_t>("chain", N);
   HIPCHK(hipMemsetAsync(d_chain, 0, N, s));
-  c->launch(K_CHAIN_SEG, k_chain_seg<16>, dim3((unsigned)std::min<int64_t>(1024, blocks(nsegs, 256))), dim3(256), s,
-            (const Unit*)d_units, d_segs, (int32_t)nsegs, (const int32_t*)d_segord, (const int32_t*)d_cord,
-            (const int32_t*)d_inv, d_par, d_exta, d_topg, d_qn, d_leaves, (const int64_t*)d_w1, d_err,
-            c->chain_stats ? c->buf<unsigned long long>("chain_stats", 8) : (unsigned long long*)nullptr);
+  // Tiers: 16-lane groups; segments whose leaf list outgrows 16 slots go to 64-lane groups,
+  // then to the lane kernel's exact global-memory path.  Each tier rewrites every output of
+  // the segments it takes.
+  int32_t* d_cnt = c->buf<int32_t>("chain_cnt", 4);
+  int32_t* d_ovf1 = c->buf<int32_t>("chain_ovf1", nsegs);
+  int32_t* d_ovf2 = c->buf<int32_t>("chain_ovf2", nsegs);
+  {
+    const int32_t cnt0[4] = {(int32_t)nsegs, 0, 0, 0};
+    HIPCHK(hipMemcpyAsync(d_cnt, cnt0, sizeof(cnt0), hipMemcpyHostToDevice, s));
+    const int32_t* list = d_segord;
+    const int32_t* nlist = d_cnt;
+    int64_t n = nsegs;
+    if (c->chain_tier <= 0) {
+      c->launch(K_CHAIN_G16, k_chain_grp<16>, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, blocks(n, 64)))),
+                dim3(256), s, (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par,
+                d_exta, d_topg, d_qn, d_ovf1, d_cnt + 1, d_err);
+      list = d_ovf1;
+      nlist = d_cnt + 1;
+      n = c->download(d_cnt + 1, 1, s)[0];
+    }
+    c->chain_tier_counts[0] = nsegs;
+    c->chain_tier_counts[1] = n;
+    if (n > 0 && c->chain_tier <= 1) {
+      c->launch(K_CHAIN_G64, k_chain_grp<64>, dim3((unsigned)blocks(n, 4)), dim3(256), s, (const Unit*)d_units, d_segs, list,
+                nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par, d_exta, d_topg, d_qn, d_ovf2, d_cnt + 2, d_err);
+      list = d_ovf2;
+      n = c->download(d_cnt + 2, 1, s)[0];
+    }
+    if (n > 0)
+      c->launch(K_CHAIN_SEG, k_chain_seg<16>, dim3((unsigned)std::min<int64_t>(1024, blocks(n, 256))), dim3(256), s,
+                (const Unit*)d_units, d_segs, (int32_t)n, list, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par,
+                d_exta, d_topg, d_qn, d_leaves, (const int64_t*)d_w1, d_err,
+                c->chain_stats ? c->buf<unsigned long long>("chain_stats", 8) : (unsigned long long*)nullptr);
+    c->chain_tier_counts[2] = n;
+  }
   int32_t* d_qexit = c->buf<int32_t>("qexit", N);
   c->launch(K_CHAIN_EXITS, k_chain_exits, dim3(blocks(nsegs, 256)), dim3(256), s, (const Unit*)d_units,
             (const Seg*)d_segs, (int32_t)nsegs, (const int32_t*)d_par, (const int32_t*)d_exta, (const int32_t*)d_qn,
@@ -905,6 +939,12 @@ int cdcx_kernel_times(cdcx_ctx* c, double* ms, int64_t* launches, int n) {
     if (ms) ms[k] = c->ktime[k];
     if (launches) launches[k] = c->klaunch[k];
   }
+  return CDCX_OK;
+}
+
+int cdcx_chain_tiers(cdcx_ctx* c, int64_t* out) {
+  if (!c || !out) return CDCX_ERR_ARG;
+  for (int k = 0; k < 3; k++) out[k] = c->chain_tier_counts[k];
   return CDCX_OK;
 }
 

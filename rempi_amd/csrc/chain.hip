@@ -266,20 +266,8 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
     } else {
       // Outside parent: resolved at stitching from (ordinal, anchor of the first leaf).
       par[a + i] = -2 - nrel1;
-      int32_t anchor = -1;
-      if (nl > 0) {
-        int32_t L, lv;
-        if (slow) {
-          const int2 e = leafg[lbase];
-          L = e.x;
-          lv = e.y;
-        } else {
-          L = lid[0];
-          lv = llv[0];
-        }
-        anchor = climb(par, a, L, lv - 1);
-      }
-      exta[a + i] = anchor;
+      // the first leaf; seg_exit climbs from it to its relative-level-1 ancestor
+      exta[a + i] = nl > 0 ? (slow ? leafg[lbase].x : lid[0]) : -1;
       nrel1++;
     }
 
@@ -379,21 +367,25 @@ template __global__ void k_chain_seg<16>(const Unit*, Seg*, int32_t, const int32
 
 // Stitching.  From a max-level node of segment s, parents lead down to a relative-level-1
 // node; its outside parent is Q[j] of segment s-1 where j is its ordinal, or, when j >= |Q|,
-// that of its anchor (an earlier relative-level-1 node), repeatedly.
+// that of its anchor -- the relative-level-1 ancestor of the segment's first leaf when the
+// node was created (exta holds that leaf) -- repeatedly.
 __device__ __forceinline__ int32_t seg_exit(const int32_t* __restrict__ par, const int32_t* __restrict__ exta,
                                             int64_t a, int32_t v, int32_t qprev, uint32_t* err) {
-  int32_t p = par[a + v];
-  while (p >= 0) {
-    v = p;
-    p = par[a + v];
-  }
-  int32_t j = -2 - p, guard = 0;
-  while (j >= qprev) {
+  int32_t guard = 0;
+  while (true) {
+    int32_t p = par[a + v];
+    while (p >= 0) {
+      v = p;
+      p = par[a + v];
+    }
+    const int32_t j = -2 - p;
+    if (j < qprev) return j;
     v = exta[a + v];
-    if (v < 0 || ++guard > (1 << 28)) { raise_error(err, kErrCorrupt); return 0; }
-    j = -2 - par[a + v];
+    if (v < 0 || ++guard > (1 << 28)) {
+      raise_error(err, kErrCorrupt);
+      return 0;
+    }
   }
-  return j;
 }
 
 // Where the chain leaves segment s (ord > 0) for each of its max-level nodes.

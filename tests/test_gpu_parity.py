@@ -143,3 +143,37 @@ def test_generator_workloads_vs_oracle(jitter, world, events, max_len):
         got = cdcx.d2h(d_out + int(off[r]), int(ln[r])).tobytes()
         assert got == want, (r, first_diff(got, want))
         assert c.decode_stream(got) == O.decode(want)
+
+
+@pytest.mark.parametrize("tier", [0, 1, 2])
+def test_chain_tiers_vs_oracle(tier, monkeypatch):
+    """Each chain tier alone (16-lane groups, 64-lane groups, lane kernel) reproduces the
+    reference bytes; the escalation path is taken when leaf lists outgrow a tier."""
+    monkeypatch.setenv("CDCX_CHAIN_TIER", str(tier))
+    c = rempi_amd.Context(131072)
+    monkeypatch.delenv("CDCX_CHAIN_TIER")
+    rng = np.random.default_rng(77 + tier)
+    bad = []
+    for t in range(60):
+        mode = ["jitter", "jitter", "jitter", "reversed", "random"][t % 5]
+        recs = S.gen_stream(int(rng.integers(1 << 30)), int(rng.integers(0, 4000)), n_sets=int(rng.integers(1, 4)),
+                            n_senders=int(rng.integers(1, 80)), jitter=int(rng.choice([0, 4, 8, 32, 200])), mode=mode)
+        want, _ = O.encode(recs, 131072)
+        got = c.encode_stream(recs)
+        if got != want:
+            bad.append((t, mode, recs.shape[0], first_diff(got, want)))
+    assert not bad, bad[:5]
+    seen = [0, 0, 0]
+    for jitter in (8, 32, 128):
+        p = rempi_amd.default_gen_params(world_size=256, jitter=jitter, events_per_rank=150000)
+        d_rec, rec_off = c.generate_device(p, 3, 2)
+        d_out, off, ln = c.encode_batch_device(d_rec, rec_off)
+        tiers = c.chain_tiers()
+        seen = [a + (b > 0) for a, b in zip(seen, tiers)]
+        for r in range(2):
+            want, _ = O.encode(rempi_amd.generate_host(p, 3 + r), 131072)
+            got = cdcx.d2h(d_out + int(off[r]), int(ln[r])).tobytes()
+            assert got == want, (jitter, r, tiers, first_diff(got, want))
+    if tier == 0:
+        assert seen[1] > 0, "no segment escalated from the 16-lane tier"
+    c.close()
