@@ -34,7 +34,7 @@ const char* kKernelNames[K_COUNT] = {
   "k_set_presence", "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_inc0", "k_tile_sum", "k_rank_scan",
   "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
-  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_window2", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records",
+  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
 
 struct HipError {
@@ -481,7 +481,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int32_t* d_fnext = c->buf<int32_t>("fnext", fk_off[R]);
   int32_t* d_fbucket = c->buf<int32_t>("fbucket", fb_off[R]);
   int32_t* d_fcount = c->buf<int32_t>("fcount", R);
-  c->launch(K_FOOTER_ORDER, k_footer_order, dim3(blocks(R, 64)), dim3(64), s, (const Unit*)d_units,
+  c->launch(K_FOOTER_ORDER, k_footer_order, dim3(R), dim3(256), s, (const Unit*)d_units,
             (const int32_t*)d_ufirst, (const int32_t*)d_nunits, (const uint64_t*)d_ep_rank, R, (const int64_t*)d_fk_off,
             (const int64_t*)d_fb_off, d_fkey, d_fnext, d_fbucket, d_fcount);
   std::vector<int32_t> fcount = c->download(d_fcount, R, s);
@@ -587,18 +587,24 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   c->dunits = units;
   uint64_t* d_wpd = c->buf<uint64_t>("d_wpd", wb);
   uint64_t* d_uidd = c->buf<uint64_t>("d_uidd", wb);
-  uint64_t* d_idd = c->buf<uint64_t>("d_idd", wb);
-  uint64_t* d_dld = c->buf<uint64_t>("d_dld", wb);
+  uint64_t* d_idd = c->buf<uint64_t>("d_idd", wb + 8);  // +8: k_dec_perm_ring reads pairs in groups of 8
+  uint64_t* d_dld = c->buf<uint64_t>("d_dld", wb + 8);
   int32_t* d_nx = c->buf<int32_t>("d_nx", wb);
   int32_t* d_pv = c->buf<int32_t>("d_pv", wb);
   int32_t* d_perm = c->buf<int32_t>("d_perm", ko);
   c->launch(K_DEC_SECTIONS, k_dec_sections, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, d_wpd, d_uidd, d_idd, d_dld);
-  // Permutation rebuild: wave per unit with a 128-slot lane window, then 256 slots, then the
-  // sequential list for whatever is left (decode.hip).
+  // Permutation rebuild: wave per unit with a 256-slot LDS ring window, then the 256-slot
+  // settle-when-full window, then the sequential list for whatever is left (decode.hip).
   int32_t* d_nfail = c->buf<int32_t>("d_nfail", 2);
   HIPCHK(hipMemsetAsync(d_nfail, 0, 8, s));
-  c->launch(K_DEC_WIN1, k_dec_perm_window<2>, dim3(NU), dim3(64), s, d_units, NU, 0, (const uint64_t*)d_idd,
-            (const uint64_t*)d_dld, d_perm, d_nfail);
+  {
+    std::vector<int32_t> order(NU);
+    for (int32_t i = 0; i < NU; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return units[a].P > units[b].P; });
+    int32_t* d_order = c->upload("d_perm_order", order, s);
+    c->launch(K_DEC_WIN1, k_dec_perm_grp, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order, NU,
+              (const uint64_t*)d_idd, (const uint64_t*)d_dld, d_perm, d_nfail);
+  }
   int32_t nf = c->download(d_nfail, 1, s)[0];
   if (nf > 0) {
     c->launch(K_DEC_WIN4, k_dec_perm_window<4>, dim3(NU), dim3(64), s, d_units, NU, 1, (const uint64_t*)d_idd,

@@ -74,6 +74,8 @@ __global__ void k_dec_units(const uint8_t*, const DChunk*, int32_t, const int32_
 __global__ void k_dec_sections(const DUnit*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*);
 __global__ void k_dec_perm_lane(const DUnit*, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*, int32_t*,
                                 uint32_t*);
+__global__ void k_dec_perm_ring(DUnit*, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
+__global__ void k_dec_perm_grp(DUnit*, const int32_t*, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
 template <int K>
 __global__ void k_dec_perm_window(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
 __global__ void k_dec_records(const DUnit*, const uint8_t*, const int32_t*, const uint64_t*, const uint64_t*,

@@ -6,6 +6,8 @@
 //   (cdc_prepare_decode_indices :1301-1386) -> per-table observed record stream.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "cdcx_device.h"
 #include "cdcx_kernels.h"
 
@@ -372,6 +374,259 @@ __global__ void __launch_bounds__(64) k_dec_perm_window(DUnit* __restrict__ unit
 
 template __global__ void k_dec_perm_window<2>(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
 template __global__ void k_dec_perm_window<4>(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
+
+// ---------------------------------------------------------------------------------------
+// Permutation rebuild, first attempt: one wave per unit, the list held as a window of
+// list positions [base, base + W) in an LDS ring, plus an LDS map element -> position for
+// the elements in the window.  Every position at or past the window still holds its
+// initial element (position q holds q): nothing has been moved there.  A pair moves x
+// from its position p to t = p + delay of the list without x, i.e. rotates the window
+// slots between p and t by one, which the lanes do as one LDS read + write per 64 slots,
+// and re-points the moved elements in the map.  The window slides forward 64 positions at
+// a time (the front 64 are settled into perm); sliding is a base increment, nothing moves.
+// All per-pair control is uniform scalar code and there is no per-slot register work, so a
+// pair costs a few scalar ops and four LDS ops.  A pair that reaches behind the window, an
+// element that is no longer in it, or a step past the list end (the std::list wrap through
+// its sentinel) marks the unit for the next attempt (k_dec_perm_window<4>, then the
+// sequential k_dec_perm_lane).
+namespace {
+constexpr int32_t kRingW = 256;   // window slots (power of two)
+constexpr int32_t kRingMap = 512; // element map entries (power of two)
+constexpr int32_t kRingAhead = 96;
+}  // namespace
+
+#define CDCX_UNI(v) __builtin_amdgcn_readfirstlane(v)
+
+__global__ void __launch_bounds__(64) k_dec_perm_ring(DUnit* __restrict__ units, const uint64_t* __restrict__ idd,
+                                                      const uint64_t* __restrict__ dld, int32_t* __restrict__ perm,
+                                                      int32_t* __restrict__ nfail) {
+  constexpr int32_t W = kRingW, WM = kRingW - 1, MM = kRingMap - 1;
+  __shared__ int32_t win[W];
+  __shared__ int2 emap[kRingMap];  // {element, absolute position}
+  const DUnit u = units[blockIdx.x];
+  if (u.fb != 0) return;
+  const int l = lane_id();
+  const int32_t M = u.M, P = u.P;
+  int32_t* pm = perm + u.key_off;
+  const uint64_t* ip = idd + u.wbase;
+  const uint64_t* dp = dld + u.wbase;
+  for (int32_t q = l; q < W; q += 64) win[q] = q;
+  for (int32_t q = l; q < kRingMap; q += 64) emap[q] = (q < W) ? make_int2(q, q) : make_int2(-1, -1);
+  int32_t base = 0;
+  int32_t fail = 0;
+  // settle [base, base+64), open [base+W, base+W+64) as identity
+#define CDCX_SLIDE()                        \
+  do {                                      \
+    const int32_t ph_ = (base + l) & WM;    \
+    const int32_t v_ = win[ph_];            \
+    if (v_ < M) pm[v_] = base + l;          \
+    const int32_t e_ = base + W + l;        \
+    win[ph_] = e_;                          \
+    emap[e_ & MM] = make_int2(e_, e_);      \
+    base = CDCX_UNI(base + 64);             \
+  } while (0)
+  for (int32_t k0 = 0; k0 < P; k0 += 8) {
+    int32_t xs[8], ds[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {  // uniform loads (scalar unit); the arrays carry 8 slack entries
+      xs[q] = (int32_t)ip[k0 + q];
+      ds[q] = (int32_t)dp[k0 + q];
+    }
+    const int32_t nk = min(8, P - k0);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      if (q >= nk) break;
+      const int32_t x = CDCX_UNI(xs[q]), d = CDCX_UNI(ds[q]);
+      if ((uint32_t)x >= (uint32_t)M) { fail = 1; break; }
+      if (x >= base + W)  // untouched, at position x: bring it kRingAhead before the window end
+        while (x >= base + W - kRingAhead) CDCX_SLIDE();
+      const int2 e = emap[x & MM];
+      int32_t p = CDCX_UNI(e.y) - base;
+      if (CDCX_UNI(e.x) != x || (uint32_t)p >= (uint32_t)W) { fail = 1; break; }
+      int32_t t = p + d;
+      if (t < 0 || base + t > M - 1) { fail = 1; break; }
+      while (t > W - 1) {
+        if (p < 64) { fail = 1; break; }
+        CDCX_SLIDE();
+        p -= 64;
+        t -= 64;
+      }
+      if (fail) break;
+      if (t >= p) {
+        // slots [p, t) take slot + 1, slot t = x; ascending 64-slot chunks
+        for (int32_t c = p; c <= t; c += 64) {
+          const int32_t s = c + l;
+          if (s <= t) {
+            const int32_t v = (s < t) ? win[(base + s + 1) & WM] : x;
+            __builtin_amdgcn_wave_barrier();
+            win[(base + s) & WM] = v;
+            emap[v & MM] = make_int2(v, base + s);
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+      } else {
+        // slots (t, p] take slot - 1, slot t = x; descending 64-slot chunks
+        for (int32_t c = p; c >= t; c -= 64) {
+          const int32_t s = c - l;
+          if (s >= t) {
+            const int32_t v = (s > t) ? win[(base + s - 1) & WM] : x;
+            __builtin_amdgcn_wave_barrier();
+            win[(base + s) & WM] = v;
+            emap[v & MM] = make_int2(v, base + s);
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+    }
+    if (fail) break;
+  }
+#undef CDCX_SLIDE
+  if (fail) {
+    if (l == 0) {
+      units[blockIdx.x].fb = 1;
+      atomicAdd(nfail, 1);
+    }
+    return;
+  }
+  for (int32_t s = l; s < W; s += 64) {
+    const int32_t v = win[(base + s) & WM];
+    if (v < M) pm[v] = base + s;
+  }
+  for (int32_t q = base + W + l; q < M; q += 64) pm[q] = q;
+}
+
+
+// ---------------------------------------------------------------------------------------
+// The same LDS-ring rebuild with one unit per 16-lane group (four units per wave).  The
+// scalar version spends ~40 scalar instructions per pair and the scalar unit is shared by
+// the CU's four SIMDs, so it is issue-bound; here the per-pair control is group-uniform
+// vector code shared by four units, and only the wave-level loops are scalar.  All groups
+// consume one pair per step (the pair index is the step count), so the q-th pair of a
+// 16-pair batch is broadcast from group lane q with DPP row_newbcast.  Units are handed
+// out longest-first (`order`) so that the four units of a wave finish together.
+namespace {
+constexpr int32_t kGW = 128;     // window slots per group (power of two)
+constexpr int32_t kGMap = 256;   // element map entries per group (power of two)
+constexpr int32_t kGAhead = 56;  // an untouched x is brought to >= kGAhead slots before the end
+
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
+template <int Q>
+__device__ __forceinline__ int32_t row_bcast(int32_t v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x150 + Q, 0xf, 0xf, false);  // row_newbcast:Q
+}
+}  // namespace
+
+__global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, const int32_t* __restrict__ order,
+                                                     int32_t n_units, const uint64_t* __restrict__ idd,
+                                                     const uint64_t* __restrict__ dld, int32_t* __restrict__ perm,
+                                                     int32_t* __restrict__ nfail) {
+  constexpr int32_t W = kGW, WM = kGW - 1, MM = kGMap - 1;
+  __shared__ int32_t win_all[4][W];
+  __shared__ int2 emap_all[4][kGMap];  // {element, absolute position}
+  const int g = threadIdx.x >> 4, j = threadIdx.x & 15;
+  int32_t* win = win_all[g];
+  int2* emap = emap_all[g];
+  const int32_t oi = blockIdx.x * 4 + g;
+  const int32_t ui = (oi < n_units) ? order[oi] : -1;
+  int32_t M = 0, P = 0;
+  int64_t wbase = 0, key_off = 0;
+  if (ui >= 0) {
+    const DUnit& u = units[ui];
+    if (u.fb == 0) {
+      M = u.M;
+      P = u.P;
+      wbase = u.wbase;
+      key_off = u.key_off;
+    }
+  }
+  int32_t* pm = perm + key_off;
+  const uint64_t* ip = idd + wbase;
+  const uint64_t* dp = dld + wbase;
+  for (int32_t q = j; q < W; q += 16) win[q] = q;
+  for (int32_t q = j; q < kGMap; q += 16) emap[q] = (q < W) ? make_int2(q, q) : make_int2(-1, -1);
+  int32_t base = 0;
+  bool fail = false;
+  const int32_t Pmax = __builtin_amdgcn_readfirstlane(wave_reduce(P, OpMax()));
+  auto slide = [&](bool go) {  // settle [base, base+16), open [base+W, base+W+16) as identity
+    if (go) {
+      const int32_t ph = (base + j) & WM;
+      const int32_t v = win[ph];
+      if (v < M) pm[v] = base + j;
+      const int32_t e = base + W + j;
+      win[ph] = e;
+      emap[e & MM] = make_int2(e, e);
+      base += 16;
+    }
+  };
+  for (int32_t k0 = 0; k0 < Pmax; k0 += 16) {
+    const bool inb = k0 + j < P;
+    const int32_t xv = inb ? (int32_t)ip[k0 + j] : 0;
+    const int32_t dv = inb ? (int32_t)dp[k0 + j] : 0;
+    static_for<16>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      if (k0 + q >= Pmax) return;
+      const int32_t x = row_bcast<q>(xv);
+      const int32_t d = row_bcast<q>(dv);
+      bool act = !fail && (k0 + q < P);
+      if (act && (uint32_t)x >= (uint32_t)M) { fail = true; act = false; }
+      // untouched x (at position x): slide until it is kGAhead slots before the window end
+      const bool far = act && x >= base + W;
+      while (__builtin_amdgcn_ballot_w64(far && x >= base + W - kGAhead)) slide(far && x >= base + W - kGAhead);
+      int2 e = make_int2(-1, -1);
+      if (act) e = emap[x & MM];
+      int32_t p = e.y - base;
+      if (act && (e.x != x || (uint32_t)p >= (uint32_t)W)) { fail = true; act = false; }
+      int32_t t = p + d;
+      if (act && (t < 0 || base + t > M - 1)) { fail = true; act = false; }
+      while (__builtin_amdgcn_ballot_w64(act && t > W - 1)) {
+        const bool go = act && t > W - 1;
+        if (go && p < 16) { fail = true; act = false; }
+        const bool sl = go && act;
+        slide(sl);
+        if (sl) {
+          p -= 16;
+          t -= 16;
+        }
+      }
+      // rotation of the slots between p and t
+      const bool fwd = t >= p;
+      const int32_t len = fwd ? t - p : p - t;
+      for (int32_t c = 0; __builtin_amdgcn_ballot_w64(act && c <= len); c += 16) {
+        const int32_t o = c + j;
+        if (act && o <= len) {
+          const int32_t s = fwd ? p + o : p - o;
+          const int32_t v = (o < len) ? win[(base + s + (fwd ? 1 : -1)) & WM] : x;
+          __builtin_amdgcn_wave_barrier();
+          win[(base + s) & WM] = v;
+          emap[v & MM] = make_int2(v, base + s);
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    });
+  }
+  if (ui >= 0 && M > 0 && P >= 0) {
+    if (fail) {
+      if (j == 0 && units[ui].fb == 0) {
+        units[ui].fb = 1;
+        atomicAdd(nfail, 1);
+      }
+    }
+  }
+  if (!fail && ui >= 0) {
+    for (int32_t s = j; s < W; s += 16) {
+      const int32_t v = win[(base + s) & WM];
+      if (v < M) pm[v] = base + s;
+    }
+    for (int32_t q = base + W + j; q < M; q += 16) pm[q] = q;
+  }
+}
 
 // Records reconstruction for one unit (decoded-record definition ii): matched row i is
 // the event of clock order c_i (c = perm^-1) with the replay-supplied sorted key; its

@@ -747,28 +747,109 @@ __global__ void __launch_bounds__(256) k_chunk_headers(const Chunk* __restrict__
 }
 
 // Footer (write_footer, :2085-2126): all_epoch_rank_uset (unordered_set<int>) fed with
-// every table's epoch ranks in emitted order; one lane per rank.
-__global__ void __launch_bounds__(64) k_footer_order(const Unit* __restrict__ units, const int32_t* __restrict__ ufirst,
-                                                     const int32_t* __restrict__ nunits, const uint64_t* __restrict__ ep_rank,
-                                                     int32_t n_ranks, const int64_t* __restrict__ fk_off,
-                                                     const int64_t* __restrict__ fb_off, uint64_t* __restrict__ fkey,
-                                                     int32_t* __restrict__ fnext, int32_t* __restrict__ fbucket,
-                                                     int32_t* __restrict__ fcount) {
-  const int r = blockIdx.x * 64 + threadIdx.x;
+// every table's epoch ranks in emitted order.  Its iteration order depends only on the
+// distinct keys in first-insertion order, so one block per rank first finds each distinct
+// key's first position (LDS hash, atomicMin of (unit, slot)), sorts the distinct keys by it,
+// and only then replays the libstdc++ insertions -- one per distinct key instead of one
+// membership walk per (table, source).  A rank with more distinct keys than the LDS hash
+// holds replays every insertion sequentially.
+__global__ void __launch_bounds__(256) k_footer_order(const Unit* __restrict__ units, const int32_t* __restrict__ ufirst,
+                                                      const int32_t* __restrict__ nunits, const uint64_t* __restrict__ ep_rank,
+                                                      int32_t n_ranks, const int64_t* __restrict__ fk_off,
+                                                      const int64_t* __restrict__ fb_off, uint64_t* __restrict__ fkey,
+                                                      int32_t* __restrict__ fnext, int32_t* __restrict__ fbucket,
+                                                      int32_t* __restrict__ fcount) {
+  constexpr int HC = 4096, LCAP = HC / 2;
+  __shared__ int32_t hkey[HC];
+  __shared__ unsigned long long hord[HC];
+  __shared__ int32_t nlist;
+  const int r = blockIdx.x;
   if (r >= n_ranks) return;
-  HashOrder ho;
-  ho.init(fkey + fk_off[r], fnext + fk_off[r], fbucket + fb_off[r]);
-  for (int32_t q = 0; q < nunits[r]; q++) {
-    const Unit u = units[ufirst[r] + q];
-    for (int32_t j = 0; j < u.S; j++) {
-      const uint64_t k = (uint64_t)(int64_t)(int32_t)ep_rank[u.a + j];
-      if (!ho.contains(k)) ho.insert_new(k);
+  for (int i = threadIdx.x; i < HC; i += 256) {
+    hkey[i] = INT32_MIN;
+    hord[i] = ~0ull;
+  }
+  if (threadIdx.x == 0) nlist = 0;
+  __syncthreads();
+  const int32_t nu = nunits[r], u0 = ufirst[r];
+  const int w = wave_id(), l = lane_id();
+  for (int32_t q = w; q < nu; q += 4) {
+    const Unit u = units[u0 + q];
+    for (int32_t j = l; j < u.S; j += 64) {
+      const int32_t k = (int32_t)ep_rank[u.a + j];
+      const unsigned long long ord = ((unsigned long long)q << 12) | (unsigned long long)j;
+      uint32_t h = ((uint32_t)k * 2654435761u) % HC;
+      for (int probe = 0; probe < HC; probe++) {
+        const int32_t old = atomicCAS(&hkey[h], INT32_MIN, k);
+        if (old == INT32_MIN) atomicAdd(&nlist, 1);
+        if (old == INT32_MIN || old == k) {
+          atomicMin(&hord[h], ord);
+          break;
+        }
+        h = (h + 1) % HC;
+      }
     }
   }
-  // Leave the iteration order in fnext's sibling array: rewrite keys in order at fkey.
-  fcount[r] = ho.size;
-  // Store the head so the writer can walk the list.
-  fbucket[fb_off[r]] = ho.head;
+  __syncthreads();
+  const int n = nlist;
+  HashOrder ho;
+  if (n > LCAP) {  // too many distinct keys for the LDS list: sequential replay
+    if (threadIdx.x == 0) {
+      ho.init(fkey + fk_off[r], fnext + fk_off[r], fbucket + fb_off[r]);
+      for (int32_t q = 0; q < nu; q++) {
+        const Unit u = units[u0 + q];
+        for (int32_t j = 0; j < u.S; j++) {
+          const uint64_t k = (uint64_t)(int64_t)(int32_t)ep_rank[u.a + j];
+          if (!ho.contains(k)) ho.insert_new(k);
+        }
+      }
+      fcount[r] = ho.size;
+      fbucket[fb_off[r]] = ho.head;
+    }
+    return;
+  }
+  // Compact into the upper half of the hash arrays' storage, then bitonic sort by order.
+  __shared__ int32_t lkey[LCAP];
+  __shared__ unsigned long long lord[LCAP];
+  __shared__ int32_t cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < HC; i += 256) {
+    if (hkey[i] != INT32_MIN) {
+      const int q = atomicAdd(&cnt, 1);
+      lkey[q] = hkey[i];
+      lord[q] = hord[i];
+    }
+  }
+  int P2 = 1;
+  while (P2 < n) P2 <<= 1;
+  __syncthreads();
+  for (int i = n + threadIdx.x; i < P2; i += 256) lord[i] = ~0ull;
+  __syncthreads();
+  for (int size = 2; size <= P2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int p = threadIdx.x; p < P2 / 2; p += 256) {
+        const int i = 2 * p - (p & (stride - 1));
+        const int j = i + stride;
+        const bool up = ((i & size) == 0);
+        if ((lord[i] > lord[j]) == up) {
+          const unsigned long long t = lord[i];
+          lord[i] = lord[j];
+          lord[j] = t;
+          const int32_t tk = lkey[i];
+          lkey[i] = lkey[j];
+          lkey[j] = tk;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) {
+    ho.init(fkey + fk_off[r], fnext + fk_off[r], fbucket + fb_off[r]);
+    for (int q = 0; q < n; q++) ho.insert_new((uint64_t)(int64_t)lkey[q]);
+    fcount[r] = ho.size;
+    fbucket[fb_off[r]] = ho.head;
+  }
 }
 
 __global__ void __launch_bounds__(64) k_footer_write(const int64_t* __restrict__ fk_off, const int64_t* __restrict__ fb_off,
