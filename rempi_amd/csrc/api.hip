@@ -93,6 +93,9 @@ struct cdcx_ctx {
   bool chain_stats = getenv("CDCX_CHAIN_STATS") != nullptr;
   // First chain tier (diagnostics / tests): 0 = 16-lane groups, 1 = 64-lane groups, 2 = lane kernel.
   int chain_tier = getenv("CDCX_CHAIN_TIER") ? atoi(getenv("CDCX_CHAIN_TIER")) : 0;
+  // First permutation-rebuild tier (diagnostics / tests): 0 = 16-lane groups, 1 = 256-slot
+  // window, 2 = sequential list.
+  int dec_tier = getenv("CDCX_DEC_TIER") ? atoi(getenv("CDCX_DEC_TIER")) : 0;
   int64_t chain_tier_counts[3] = {0, 0, 0};  // segments entering each tier in the last encode
 
   template <class T>
@@ -581,20 +584,26 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
     wb += (int64_t)u.M + 1;
     ro += (int64_t)u.M + (u.Uc > 0 ? u.U : 0);
     ko += u.M;
+    u.fb = std::min(std::max(c->dec_tier, 0), 2);
   }
   if (records && n_keys < ko) throw CdcxError{CDCX_ERR_ARG, "fewer sorted keys than matched events in the files"};
   d_units = c->upload("d_units", units, s);
   c->dunits = units;
   uint64_t* d_wpd = c->buf<uint64_t>("d_wpd", wb);
   uint64_t* d_uidd = c->buf<uint64_t>("d_uidd", wb);
-  uint64_t* d_idd = c->buf<uint64_t>("d_idd", wb + 8);  // +8: k_dec_perm_ring reads pairs in groups of 8
-  uint64_t* d_dld = c->buf<uint64_t>("d_dld", wb + 8);
+  uint64_t* d_idd = c->buf<uint64_t>("d_idd", wb);  // written by k_dec_perm_grp
+  uint64_t* d_dld = c->buf<uint64_t>("d_dld", wb);
   int32_t* d_nx = c->buf<int32_t>("d_nx", wb);
   int32_t* d_pv = c->buf<int32_t>("d_pv", wb);
   int32_t* d_perm = c->buf<int32_t>("d_perm", ko);
-  c->launch(K_DEC_SECTIONS, k_dec_sections, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, d_wpd, d_uidd, d_idd, d_dld);
-  // Permutation rebuild: wave per unit with a 256-slot LDS ring window, then the 256-slot
-  // settle-when-full window, then the sequential list for whatever is left (decode.hip).
+  uint8_t* d_wnf = c->buf<uint8_t>("d_wnf", wb);
+  HIPCHK(hipMemsetAsync(d_wnf, 0, wb, s));
+  c->launch(K_DEC_SECTIONS, k_dec_sections, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, d_wpd, d_uidd, d_wnf,
+            d_err);
+  // Permutation rebuild (decode.hip): 16-lane groups with LDS ring windows, which also invert
+  // the pair sections' LP; then the 256-slot settle-when-full window, then the sequential
+  // list for whatever is left.
+  int32_t* d_cinv = c->buf<int32_t>("d_cinv", ko);
   int32_t* d_nfail = c->buf<int32_t>("d_nfail", 2);
   HIPCHK(hipMemsetAsync(d_nfail, 0, 8, s));
   {
@@ -602,17 +611,19 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
     for (int32_t i = 0; i < NU; i++) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return units[a].P > units[b].P; });
     int32_t* d_order = c->upload("d_perm_order", order, s);
-    c->launch(K_DEC_WIN1, k_dec_perm_grp, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order, NU,
-              (const uint64_t*)d_idd, (const uint64_t*)d_dld, d_perm, d_nfail);
+    c->launch(K_DEC_WIN1, k_dec_perm_grp, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order, NU, d_in,
+              d_idd, d_dld, d_perm, d_cinv, d_nfail);
   }
-  int32_t nf = c->download(d_nfail, 1, s)[0];
+  int32_t nf = c->dec_tier > 0 ? NU : c->download(d_nfail, 1, s)[0];
   if (nf > 0) {
     c->launch(K_DEC_WIN4, k_dec_perm_window<4>, dim3(NU), dim3(64), s, d_units, NU, 1, (const uint64_t*)d_idd,
               (const uint64_t*)d_dld, d_perm, d_nfail + 1);
-    nf = c->download(d_nfail + 1, 1, s)[0];
-    if (nf > 0)
+    const int32_t nf2 = c->dec_tier > 1 ? NU : c->download(d_nfail + 1, 1, s)[0];
+    if (nf2 > 0)
       c->launch(K_DEC_PERM, k_dec_perm_lane, dim3(blocks(NU, 64)), dim3(64), s, (const DUnit*)d_units, NU,
                 (const uint64_t*)d_idd, (const uint64_t*)d_dld, d_nx, d_pv, d_perm, d_err);
+    c->launch(K_DEC_PERM, k_dec_cinv, dim3(NU), dim3(256), s, (const DUnit*)d_units, (const int32_t*)d_perm, d_cinv);
+    nf = nf2;
   }
   c->last_fallback_units = nf;
   c->check_err(d_err, s);
@@ -621,11 +632,18 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   c->d_perm = d_perm;
   c->n_rec_out = ro;
   if (records) {
-    int32_t* d_cinv = c->buf<int32_t>("d_cinv", wb);
-    uint8_t* d_wnf = c->buf<uint8_t>("d_wnf", wb);
+    std::vector<int2> rt;
+    for (int32_t q = 0; q < NU; q++) {
+      const DUnit& u = units[q];
+      if (u.M == 0 && (u.Uc == 0 || u.U == 0)) continue;
+      const int32_t nt = std::max<int32_t>(1, (u.M + 1023) / 1024);
+      for (int32_t k = 0; k < nt; k++) rt.push_back(make_int2(q, k));
+    }
+    int2* d_rt = c->upload("d_rec_tiles", rt, s);
     int32_t* d_recs = c->buf<int32_t>("d_recs", 8 * ro);
-    c->launch(K_DEC_RECORDS, k_dec_records, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, (const int32_t*)d_perm,
-              (const uint64_t*)d_wpd, (const uint64_t*)d_uidd, d_keys, d_cinv, d_wnf, (int4*)d_recs, d_err);
+    c->launch(K_DEC_RECORDS, k_dec_records, dim3((unsigned)rt.size()), dim3(256), s, (const DUnit*)d_units,
+              (const int2*)d_rt, d_in, (const int32_t*)d_cinv, (const uint8_t*)d_wnf, (const uint64_t*)d_uidd, d_keys,
+              (int4*)d_recs);
     c->check_err(d_err, s);
     c->d_rec_out = d_recs;
   }

@@ -71,15 +71,16 @@ __global__ void k_write_keys(const Unit*, const uint64_t*, int2*);
 __global__ void k_dec_count_chunks(const uint8_t*, const int64_t*, const int64_t*, int32_t, int32_t*, uint32_t*);
 __global__ void k_dec_list_chunks(const uint8_t*, const int64_t*, const int32_t*, const int32_t*, int32_t, DChunk*);
 __global__ void k_dec_units(const uint8_t*, const DChunk*, int32_t, const int32_t*, int32_t*, DUnit*, uint32_t*);
-__global__ void k_dec_sections(const DUnit*, const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*);
+__global__ void k_dec_sections(const DUnit*, const uint8_t*, uint64_t*, uint64_t*, uint8_t*, uint32_t*);
 __global__ void k_dec_perm_lane(const DUnit*, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*, int32_t*,
                                 uint32_t*);
-__global__ void k_dec_perm_ring(DUnit*, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
-__global__ void k_dec_perm_grp(DUnit*, const int32_t*, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
+__global__ void k_dec_perm_grp(DUnit*, const int32_t*, int32_t, const uint8_t*, uint64_t*, uint64_t*, int32_t*, int32_t*,
+                               int32_t*);
+__global__ void k_dec_cinv(const DUnit*, const int32_t*, int32_t*);
 template <int K>
 __global__ void k_dec_perm_window(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
-__global__ void k_dec_records(const DUnit*, const uint8_t*, const int32_t*, const uint64_t*, const uint64_t*,
-                              const int2*, int32_t*, uint8_t*, int4*, uint32_t*);
+__global__ void k_dec_records(const DUnit*, const int2*, const uint8_t*, const int32_t*, const uint8_t*, const uint64_t*,
+                              const int2*, int4*);
 
 // gen.hip
 __global__ void k_gen_tile_sums(GenArgs, int64_t, int32_t, int32_t*, int32_t*);

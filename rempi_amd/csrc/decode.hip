@@ -140,15 +140,29 @@ __device__ void inverse_lp(const uint8_t* __restrict__ src, int32_t n, uint64_t*
   }
 }
 
+// with_previous and unmatched-id sections (the pair sections are inverted by the
+// permutation kernel as it consumes them).  Also: the with_next flag of every matched row
+// (with_previous_bool_vec, :1104-1110; wnf must be zeroed) and the unmatched-id checks of
+// the records stage (ids strictly increasing and <= count), so that later kernels can
+// binary-search the id list.
 __global__ void __launch_bounds__(256) k_dec_sections(const DUnit* __restrict__ units, const uint8_t* __restrict__ in,
                                                       uint64_t* __restrict__ wpd, uint64_t* __restrict__ uidd,
-                                                      uint64_t* __restrict__ idd, uint64_t* __restrict__ dld) {
+                                                      uint8_t* __restrict__ wnf, uint32_t* err) {
   __shared__ uint64_t lds[4];
   const DUnit u = units[blockIdx.x];
   inverse_lp<false>(in + u.wp_off, u.W, wpd + u.wbase, lds);
   inverse_lp<false>(in + u.uid_off, u.U, uidd + u.wbase, lds);
-  inverse_lp<true>(in + u.pair_off, u.P, idd + u.wbase, lds);
-  inverse_lp<true>(in + u.pair_off + 4ll * u.P, u.P, dld + u.wbase, lds);
+  __syncthreads();
+  for (int32_t k = threadIdx.x; k < u.W; k += 256) {
+    const uint64_t w = wpd[u.wbase + k];
+    if (w >= (uint64_t)u.M) raise_error(err, kErrCorrupt);
+    else wnf[u.wbase + w] = 1;
+  }
+  if (u.Uc > 0) {
+    const uint64_t* ids = uidd + u.wbase;
+    for (int32_t k = threadIdx.x; k < u.U; k += 256)
+      if (ids[k] > (uint64_t)u.M || (k > 0 && ids[k] <= ids[k - 1])) raise_error(err, kErrCorrupt);
+  }
 }
 
 // cdc_prepare_decode_indices, one lane per unit: the list 0..M-1 (+ sentinel M, circular
@@ -376,134 +390,27 @@ template __global__ void k_dec_perm_window<2>(DUnit*, int32_t, int32_t, const ui
 template __global__ void k_dec_perm_window<4>(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
 
 // ---------------------------------------------------------------------------------------
-// Permutation rebuild, first attempt: one wave per unit, the list held as a window of
-// list positions [base, base + W) in an LDS ring, plus an LDS map element -> position for
-// the elements in the window.  Every position at or past the window still holds its
-// initial element (position q holds q): nothing has been moved there.  A pair moves x
-// from its position p to t = p + delay of the list without x, i.e. rotates the window
-// slots between p and t by one, which the lanes do as one LDS read + write per 64 slots,
-// and re-points the moved elements in the map.  The window slides forward 64 positions at
-// a time (the front 64 are settled into perm); sliding is a base increment, nothing moves.
-// All per-pair control is uniform scalar code and there is no per-slot register work, so a
-// pair costs a few scalar ops and four LDS ops.  A pair that reaches behind the window, an
-// element that is no longer in it, or a step past the list end (the std::list wrap through
-// its sentinel) marks the unit for the next attempt (k_dec_perm_window<4>, then the
-// sequential k_dec_perm_lane).
-namespace {
-constexpr int32_t kRingW = 256;   // window slots (power of two)
-constexpr int32_t kRingMap = 512; // element map entries (power of two)
-constexpr int32_t kRingAhead = 96;
-}  // namespace
-
-#define CDCX_UNI(v) __builtin_amdgcn_readfirstlane(v)
-
-__global__ void __launch_bounds__(64) k_dec_perm_ring(DUnit* __restrict__ units, const uint64_t* __restrict__ idd,
-                                                      const uint64_t* __restrict__ dld, int32_t* __restrict__ perm,
-                                                      int32_t* __restrict__ nfail) {
-  constexpr int32_t W = kRingW, WM = kRingW - 1, MM = kRingMap - 1;
-  __shared__ int32_t win[W];
-  __shared__ int2 emap[kRingMap];  // {element, absolute position}
-  const DUnit u = units[blockIdx.x];
-  if (u.fb != 0) return;
-  const int l = lane_id();
-  const int32_t M = u.M, P = u.P;
-  int32_t* pm = perm + u.key_off;
-  const uint64_t* ip = idd + u.wbase;
-  const uint64_t* dp = dld + u.wbase;
-  for (int32_t q = l; q < W; q += 64) win[q] = q;
-  for (int32_t q = l; q < kRingMap; q += 64) emap[q] = (q < W) ? make_int2(q, q) : make_int2(-1, -1);
-  int32_t base = 0;
-  int32_t fail = 0;
-  // settle [base, base+64), open [base+W, base+W+64) as identity
-#define CDCX_SLIDE()                        \
-  do {                                      \
-    const int32_t ph_ = (base + l) & WM;    \
-    const int32_t v_ = win[ph_];            \
-    if (v_ < M) pm[v_] = base + l;          \
-    const int32_t e_ = base + W + l;        \
-    win[ph_] = e_;                          \
-    emap[e_ & MM] = make_int2(e_, e_);      \
-    base = CDCX_UNI(base + 64);             \
-  } while (0)
-  for (int32_t k0 = 0; k0 < P; k0 += 8) {
-    int32_t xs[8], ds[8];
-#pragma unroll
-    for (int q = 0; q < 8; q++) {  // uniform loads (scalar unit); the arrays carry 8 slack entries
-      xs[q] = (int32_t)ip[k0 + q];
-      ds[q] = (int32_t)dp[k0 + q];
-    }
-    const int32_t nk = min(8, P - k0);
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      if (q >= nk) break;
-      const int32_t x = CDCX_UNI(xs[q]), d = CDCX_UNI(ds[q]);
-      if ((uint32_t)x >= (uint32_t)M) { fail = 1; break; }
-      if (x >= base + W)  // untouched, at position x: bring it kRingAhead before the window end
-        while (x >= base + W - kRingAhead) CDCX_SLIDE();
-      const int2 e = emap[x & MM];
-      int32_t p = CDCX_UNI(e.y) - base;
-      if (CDCX_UNI(e.x) != x || (uint32_t)p >= (uint32_t)W) { fail = 1; break; }
-      int32_t t = p + d;
-      if (t < 0 || base + t > M - 1) { fail = 1; break; }
-      while (t > W - 1) {
-        if (p < 64) { fail = 1; break; }
-        CDCX_SLIDE();
-        p -= 64;
-        t -= 64;
-      }
-      if (fail) break;
-      if (t >= p) {
-        // slots [p, t) take slot + 1, slot t = x; ascending 64-slot chunks
-        for (int32_t c = p; c <= t; c += 64) {
-          const int32_t s = c + l;
-          if (s <= t) {
-            const int32_t v = (s < t) ? win[(base + s + 1) & WM] : x;
-            __builtin_amdgcn_wave_barrier();
-            win[(base + s) & WM] = v;
-            emap[v & MM] = make_int2(v, base + s);
-          }
-          __builtin_amdgcn_wave_barrier();
-        }
-      } else {
-        // slots (t, p] take slot - 1, slot t = x; descending 64-slot chunks
-        for (int32_t c = p; c >= t; c -= 64) {
-          const int32_t s = c - l;
-          if (s >= t) {
-            const int32_t v = (s > t) ? win[(base + s - 1) & WM] : x;
-            __builtin_amdgcn_wave_barrier();
-            win[(base + s) & WM] = v;
-            emap[v & MM] = make_int2(v, base + s);
-          }
-          __builtin_amdgcn_wave_barrier();
-        }
-      }
-    }
-    if (fail) break;
-  }
-#undef CDCX_SLIDE
-  if (fail) {
-    if (l == 0) {
-      units[blockIdx.x].fb = 1;
-      atomicAdd(nfail, 1);
-    }
-    return;
-  }
-  for (int32_t s = l; s < W; s += 64) {
-    const int32_t v = win[(base + s) & WM];
-    if (v < M) pm[v] = base + s;
-  }
-  for (int32_t q = base + W + l; q < M; q += 64) pm[q] = q;
-}
-
-
-// ---------------------------------------------------------------------------------------
-// The same LDS-ring rebuild with one unit per 16-lane group (four units per wave).  The
-// scalar version spends ~40 scalar instructions per pair and the scalar unit is shared by
-// the CU's four SIMDs, so it is issue-bound; here the per-pair control is group-uniform
-// vector code shared by four units, and only the wave-level loops are scalar.  All groups
-// consume one pair per step (the pair index is the step count), so the q-th pair of a
-// 16-pair batch is broadcast from group lane q with DPP row_newbcast.  Units are handed
-// out longest-first (`order`) so that the four units of a wave finish together.
+// Permutation rebuild, first attempt: one unit per 16-lane group (four units per wave).
+// The list is held as a window of list positions [base, base + W) in a per-group LDS ring,
+// plus an LDS map element -> position for the elements in the window.  Every position at
+// or past the window still holds its initial element (position q holds q): nothing has
+// been moved there.  A pair moves x from its position p to t = p + delay of the list
+// without x, i.e. rotates the window slots between p and t by one: one LDS read + write
+// per 16 slots across the group's lanes, and the moved elements are re-pointed in the map.
+// The window slides forward 16 positions at a time (the front 16 are settled into perm and
+// its inverse cinv); sliding is a base increment, nothing moves.
+//
+// Why groups: with one unit per wave the per-pair control is scalar code (~40 SALU per
+// pair) and the scalar unit is shared by the CU's four SIMDs, so that version is bound by
+// scalar issue; here the per-pair control is group-uniform vector code shared by four
+// units.  All groups consume one pair per step (the pair index is the step count), so the
+// q-th pair of a 16-pair batch is broadcast from group lane q with DPP row_newbcast.  Units
+// are handed out longest-first (`order`) so that the four units of a wave finish together.
+// The pair sections' inverse LP (two chained prefix sums) is done here, 16 pairs at a time.
+//
+// A pair that reaches behind the window, an element no longer in it, or a step past the
+// list end (the std::list wrap through its sentinel) marks the unit for the next attempt
+// (k_dec_perm_window<4>, then the sequential k_dec_perm_lane).
 namespace {
 constexpr int32_t kGW = 128;     // window slots per group (power of two)
 constexpr int32_t kGMap = 256;   // element map entries per group (power of two)
@@ -517,6 +424,16 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+__device__ __forceinline__ int64_t row_incl_scan64(int64_t v) {  // inclusive scan over a 16-lane row
+  const int j = threadIdx.x & 15;
+#pragma unroll
+  for (int d = 1; d < 16; d <<= 1) {
+    const int64_t o = __shfl_up(v, d, 16);
+    if (j >= d) v += o;
+  }
+  return v;
+}
+
 template <int Q>
 __device__ __forceinline__ int32_t row_bcast(int32_t v) {
   return __builtin_amdgcn_update_dpp(0, v, 0x150 + Q, 0xf, 0xf, false);  // row_newbcast:Q
@@ -524,8 +441,9 @@ __device__ __forceinline__ int32_t row_bcast(int32_t v) {
 }  // namespace
 
 __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, const int32_t* __restrict__ order,
-                                                     int32_t n_units, const uint64_t* __restrict__ idd,
-                                                     const uint64_t* __restrict__ dld, int32_t* __restrict__ perm,
+                                                     int32_t n_units, const uint8_t* __restrict__ in,
+                                                     uint64_t* __restrict__ idd, uint64_t* __restrict__ dld,
+                                                     int32_t* __restrict__ perm, int32_t* __restrict__ cinv,
                                                      int32_t* __restrict__ nfail) {
   constexpr int32_t W = kGW, WM = kGW - 1, MM = kGMap - 1;
   __shared__ int32_t win_all[4][W];
@@ -536,29 +454,37 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
   const int32_t oi = blockIdx.x * 4 + g;
   const int32_t ui = (oi < n_units) ? order[oi] : -1;
   int32_t M = 0, P = 0;
-  int64_t wbase = 0, key_off = 0;
+  int64_t wbase = 0, key_off = 0, pair_off = 0;
+  bool sim = false;  // units already marked for a later tier only get their pairs' LP inverted
   if (ui >= 0) {
     const DUnit& u = units[ui];
-    if (u.fb == 0) {
-      M = u.M;
-      P = u.P;
-      wbase = u.wbase;
-      key_off = u.key_off;
-    }
+    sim = (u.fb == 0);
+    M = u.M;
+    P = u.P;
+    wbase = u.wbase;
+    key_off = u.key_off;
+    pair_off = u.pair_off;
   }
   int32_t* pm = perm + key_off;
-  const uint64_t* ip = idd + wbase;
-  const uint64_t* dp = dld + wbase;
+  int32_t* ci = cinv + key_off;
+  uint64_t* ip = idd + wbase;
+  uint64_t* dp = dld + wbase;
+  const int32_t* yid = reinterpret_cast<const int32_t*>(in + pair_off);
+  const int32_t* ydl = yid + P;
+  int64_t czi = 0, cxi = 0, czd = 0, cxd = 0;  // inverse-LP carries (rempi_compression_util.cpp:157-168)
   for (int32_t q = j; q < W; q += 16) win[q] = q;
   for (int32_t q = j; q < kGMap; q += 16) emap[q] = (q < W) ? make_int2(q, q) : make_int2(-1, -1);
   int32_t base = 0;
-  bool fail = false;
+  bool fail = !sim;
   const int32_t Pmax = __builtin_amdgcn_readfirstlane(wave_reduce(P, OpMax()));
   auto slide = [&](bool go) {  // settle [base, base+16), open [base+W, base+W+16) as identity
     if (go) {
       const int32_t ph = (base + j) & WM;
       const int32_t v = win[ph];
-      if (v < M) pm[v] = base + j;
+      if (v < M) {
+        pm[v] = base + j;
+        ci[base + j] = v;
+      }
       const int32_t e = base + W + j;
       win[ph] = e;
       emap[e & MM] = make_int2(e, e);
@@ -566,9 +492,22 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
     }
   };
   for (int32_t k0 = 0; k0 < Pmax; k0 += 16) {
+    // inverse LP of the next 16 pairs: x = prefix(prefix(y)) of the sign-extended int32
+    // sections, mod 2^64 (decode :1004-1014 + :157-168); the sim uses the low 32 bits
     const bool inb = k0 + j < P;
-    const int32_t xv = inb ? (int32_t)ip[k0 + j] : 0;
-    const int32_t dv = inb ? (int32_t)dp[k0 + j] : 0;
+    const int64_t yi = inb ? (int64_t)yid[k0 + j] : 0, yd = inb ? (int64_t)ydl[k0 + j] : 0;
+    const int64_t zi = row_incl_scan64(yi), zd = row_incl_scan64(yd);
+    const int64_t xi = cxi + (int64_t)(j + 1) * czi + row_incl_scan64(zi);
+    const int64_t xd = cxd + (int64_t)(j + 1) * czd + row_incl_scan64(zd);
+    czi += __shfl(zi, 15, 16);
+    czd += __shfl(zd, 15, 16);
+    cxi = __shfl(xi, 15, 16);
+    cxd = __shfl(xd, 15, 16);
+    if (inb) {
+      ip[k0 + j] = (uint64_t)xi;
+      dp[k0 + j] = (uint64_t)xd;
+    }
+    const int32_t xv = (int32_t)xi, dv = (int32_t)xd;
     static_for<16>([&](auto qc) {
       constexpr int q = decltype(qc)::value;
       if (k0 + q >= Pmax) return;
@@ -611,68 +550,101 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
       }
     });
   }
-  if (ui >= 0 && M > 0 && P >= 0) {
-    if (fail) {
-      if (j == 0 && units[ui].fb == 0) {
-        units[ui].fb = 1;
-        atomicAdd(nfail, 1);
-      }
-    }
+  if (sim && fail && j == 0) {
+    units[ui].fb = 1;
+    atomicAdd(nfail, 1);
   }
-  if (!fail && ui >= 0) {
+  if (!fail) {
     for (int32_t s = j; s < W; s += 16) {
       const int32_t v = win[(base + s) & WM];
-      if (v < M) pm[v] = base + s;
+      if (v < M) {
+        pm[v] = base + s;
+        ci[base + s] = v;
+      }
     }
-    for (int32_t q = base + W + j; q < M; q += 16) pm[q] = q;
+    for (int32_t q = base + W + j; q < M; q += 16) {
+      pm[q] = q;
+      ci[q] = q;
+    }
   }
 }
 
-// Records reconstruction for one unit (decoded-record definition ii): matched row i is
-// the event of clock order c_i (c = perm^-1) with the replay-supplied sorted key; its
-// with_next comes from with_previous, its index from matched_index; unmatched run k with
-// id `id` sits right before matched row `id`.
-__global__ void __launch_bounds__(256) k_dec_records(const DUnit* __restrict__ units, const uint8_t* __restrict__ in,
-                                                     const int32_t* __restrict__ perm, const uint64_t* __restrict__ wpd,
-                                                     const uint64_t* __restrict__ uidd, const int2* __restrict__ keys,
-                                                     int32_t* __restrict__ cinv, uint8_t* __restrict__ wnf,
-                                                     int4* __restrict__ rec, uint32_t* err) {
+// Rows whose permutation came from the fallback kernels: c = perm^-1.
+__global__ void __launch_bounds__(256) k_dec_cinv(const DUnit* __restrict__ units, const int32_t* __restrict__ perm,
+                                                  int32_t* __restrict__ cinv) {
   const DUnit u = units[blockIdx.x];
+  if (u.fb == 0) return;
+  for (int32_t v = threadIdx.x; v < u.M; v += 256) cinv[u.key_off + perm[u.key_off + v]] = v;
+}
+
+// Records reconstruction (decoded-record definition ii), one block per 1024-row tile of a
+// unit: matched row i is the event of clock order c_i (cinv, written by the permutation
+// rebuild) with the replay-supplied sorted key; with_next from the row flags, index from
+// matched_index; unmatched run k with id `id` sits right before matched row `id`, so row
+// i lands at i + #runs with id <= i.  The run ids were checked strictly increasing by
+// k_dec_sections, so a tile finds its runs by binary search and ranks rows with one scan.
+__global__ void __launch_bounds__(256) k_dec_records(const DUnit* __restrict__ units, const int2* __restrict__ tiles,
+                                                     const uint8_t* __restrict__ in, const int32_t* __restrict__ cinv,
+                                                     const uint8_t* __restrict__ wnf, const uint64_t* __restrict__ uidd,
+                                                     const int2* __restrict__ keys, int4* __restrict__ rec) {
+  constexpr int TR = 1024, PER = TR / 256;
+  __shared__ int32_t mk[TR + 1];
+  __shared__ int32_t rlo, rhi;
+  __shared__ int32_t lds[4];
+  const int2 T = tiles[blockIdx.x];
+  const DUnit u = units[T.x];
   const int32_t M = u.M;
   const int32_t U = (u.Uc > 0) ? u.U : 0;
-  int32_t* ci = cinv + u.wbase;
-  uint8_t* wf = wnf + u.wbase;
-  for (int32_t v = threadIdx.x; v < M; v += 256) {
-    ci[perm[u.key_off + v]] = v;
-    wf[v] = 0;
+  const int32_t i0 = T.y * TR;
+  const int32_t n = max(0, min(TR, M - i0));
+  const bool last = i0 + TR >= M;
+  const uint64_t* ids = uidd + u.wbase;
+  for (int r = threadIdx.x; r <= TR; r += 256) mk[r] = 0;
+  if (threadIdx.x < 2) {
+    const uint64_t key = (threadIdx.x == 0) ? (uint64_t)i0 : (last ? (uint64_t)M + 1 : (uint64_t)(i0 + TR));
+    int32_t lo = 0, hi = U;
+    while (lo < hi) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (ids[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    if (threadIdx.x == 0) rlo = lo; else rhi = lo;
   }
   __syncthreads();
-  for (int32_t k = threadIdx.x; k < u.W; k += 256) {
-    const uint64_t w = wpd[u.wbase + k];
-    if (w >= (uint64_t)M) raise_error(err, kErrCorrupt);
-    else wf[w] = 1;
-  }
-  const uint64_t* ids = uidd + u.wbase;
-  for (int32_t k = threadIdx.x; k < U; k += 256) {
-    if (ids[k] > (uint64_t)M || (k > 0 && ids[k] <= ids[k - 1])) { raise_error(err, kErrCorrupt); continue; }
-    const int64_t at = u.rec_off + (int64_t)ids[k] + k;
+  const int32_t lo = rlo, hi = rhi;
+  for (int32_t k = lo + threadIdx.x; k < hi; k += 256) {
+    const int32_t id = (int32_t)ids[k];
+    mk[id - i0] = 1;
+    const int64_t at = u.rec_off + id + k;
     const int32_t cnt = (int32_t)ld_u64(in + u.ucnt_off + 8ll * k);
     rec[2 * at] = make_int4(cnt, 2, 0, 0);
     rec[2 * at + 1] = make_int4(0, 0, 0, u.set_id);
   }
   __syncthreads();
-  for (int32_t i = threadIdx.x; i < M; i += 256) {
-    int32_t lo = 0, hi = U;  // runs with id <= i
-    while (lo < hi) {
-      const int32_t mid = (lo + hi) >> 1;
-      if (ids[mid] <= (uint64_t)i) lo = mid + 1; else hi = mid;
-    }
-    const int64_t at = u.rec_off + i + lo;
-    const int2 k = keys[u.key_off + ci[i]];
+  // runs before row r (inclusive of a run with id == r): scan in thread-contiguous order,
+  // then rows are written lane-contiguous so that each store instruction covers 2 KiB
+  int32_t tot = 0;
+#pragma unroll
+  for (int q = 0; q < PER; q++) tot += mk[threadIdx.x * PER + q];
+  int32_t all;
+  int32_t run = block_exclusive_scan<256>(tot, 0, OpAdd(), lds, &all) + lo;
+#pragma unroll
+  for (int q = 0; q < PER; q++) {
+    run += mk[threadIdx.x * PER + q];
+    mk[threadIdx.x * PER + q] = run;  // each thread rewrites only its own entries
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < PER; q++) {
+    const int32_t r = q * 256 + threadIdx.x;
+    if (r >= n) break;
+    const int32_t i = i0 + r;
+    const int64_t at = u.rec_off + i + mk[r];
+    const int2 k = keys[u.key_off + cinv[u.key_off + i]];
     const int32_t idx = (int32_t)ld_u64(in + u.mi_off + 8ll * i);
     rec[2 * at] = make_int4(1, 2, 1, k.x);
-    rec[2 * at + 1] = make_int4(wf[i], idx, k.y, u.set_id);
+    rec[2 * at + 1] = make_int4(wnf[u.wbase + i], idx, k.y, u.set_id);
   }
+}
 }
 
 }  // namespace cdcx
