@@ -645,6 +645,5 @@ __global__ void __launch_bounds__(256) k_dec_records(const DUnit* __restrict__ u
     rec[2 * at + 1] = make_int4(wnf[u.wbase + i], idx, k.y, u.set_id);
   }
 }
-}
 
 }  // namespace cdcx
