@@ -447,16 +447,17 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   c->launch(K_CHAIN_MARK, k_chain_mark, dim3(blocks(nsegs, 256)), dim3(256), s, (const Unit*)d_units,
             (const Seg*)d_segs, (int32_t)nsegs, (const int32_t*)d_par, (const int32_t*)d_qn, d_chain);
   int32_t* d_posA = c->buf<int32_t>("posA", N);
-  int32_t* d_posR = c->buf<int32_t>("posR", N);
+  int32_t* d_crow = c->buf<int32_t>("crow", N);
   uint32_t* d_seq = c->buf<uint32_t>("seq", 2 * N);
-  int32_t* d_sidx = c->buf<int32_t>("sidx", 2 * N);
-  c->launch(K_POSITIONS, k_positions, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_cord,
-            (const int32_t*)d_inv, (const uint8_t*)d_chain, d_posA, d_posR, d_seq, d_sidx);
+  int32_t* d_sx = c->buf<int32_t>("sx", 2 * N);
+  c->launch(K_POSITIONS, k_pos_rows, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_cord,
+            (const uint8_t*)d_chain, d_posA, d_crow, d_seq);
+  c->launch(K_POSITIONS, k_pos_cols, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_inv,
+            (const uint8_t*)d_chain, (const int32_t*)d_posA, (const int32_t*)d_crow, d_seq, d_sx);
   int32_t* d_pid = c->buf<int32_t>("pid", N);
   int32_t* d_pdl = c->buf<int32_t>("pdl", N);
-  c->launch(K_DELTAS, k_deltas, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_cord,
-            (const uint8_t*)d_chain, (const int32_t*)d_posA, (const int32_t*)d_posR, (const uint32_t*)d_seq,
-            (const int32_t*)d_sidx, d_pid, d_pdl);
+  c->launch(K_DELTAS, k_deltas, dim3(NU), dim3(256), s, (const Unit*)d_units, (const uint32_t*)d_seq, (const int32_t*)d_sx,
+            d_pid, d_pdl);
   c->check_err(d_err, s);
   units = c->download(d_units, NU, s);
 

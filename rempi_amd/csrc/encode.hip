@@ -558,119 +558,184 @@ __global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const u
 // after column j (M for the end).  seq[2a+pos] = partner position << 2 | type.
 enum : uint32_t { kIgn = 0, kAdd = 1, kRem = 2 };
 
-__global__ void __launch_bounds__(256) k_positions(const Unit* __restrict__ units, const int32_t* __restrict__ cord,
-                                                   const int32_t* __restrict__ inv, const uint8_t* __restrict__ chain,
-                                                   int32_t* __restrict__ posA, int32_t* __restrict__ posR,
-                                                   uint32_t* __restrict__ seq, int32_t* __restrict__ sidx) {
-  __shared__ int32_t lds[4];
+namespace {
+// Block-wide exclusive scan of (count, max) pairs for 256 threads.
+__device__ __forceinline__ int2 block_scan_cnt_max(int2 v, int2* lds, int2* total) {
+  const int l = lane_id(), w = wave_id();
+  int2 inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t ox = __shfl_up(inc.x, d, 64), oy = __shfl_up(inc.y, d, 64);
+    if (l >= d) {
+      inc.x += ox;
+      inc.y = max(inc.y, oy);
+    }
+  }
+  if (l == 63) lds[w] = inc;
+  __syncthreads();
+  int2 pre = make_int2(0, INT32_MIN);
+  for (int q = 0; q < w; q++) {
+    pre.x += lds[q].x;
+    pre.y = max(pre.y, lds[q].y);
+  }
+  int2 tot = pre;
+  for (int q = w; q < 4; q++) {
+    tot.x += lds[q].x;
+    tot.y = max(tot.y, lds[q].y);
+  }
+  int32_t ex = __shfl_up(inc.x, 1, 64), ey = __shfl_up(inc.y, 1, 64);
+  if (l == 0) {
+    ex = 0;
+    ey = INT32_MIN;
+  }
+  *total = tot;
+  __syncthreads();
+  return make_int2(pre.x + ex, max(pre.y, ey));
+}
+}  // namespace
+
+// Rows pass (4 rows per thread per round): Kr = #chain rows before r, colprev = last chain
+// column before r.  posA of the IGNORE of chain row r / the ADD of off-chain row r (see
+// above), crow[k] = row of the k-th chain node, and the IGNORE entries of the sequence.
+__global__ void __launch_bounds__(256) k_pos_rows(const Unit* __restrict__ units, const int32_t* __restrict__ cord,
+                                                  const uint8_t* __restrict__ chain, int32_t* __restrict__ posA,
+                                                  int32_t* __restrict__ crow, uint32_t* __restrict__ seq) {
+  __shared__ int2 lds[4];
   const Unit u = units[blockIdx.x];
   const int64_t a = u.a;
   const int32_t M = u.M;
   const int32_t* c = cord + a;
-  const int32_t* iv = inv + a;
   const uint8_t* ch = chain + a;
-  // rows
-  int32_t ck = 0, cc = -1;
-  for (int32_t b = 0; b < M; b += 256) {
-    const int32_t r = b + threadIdx.x;
-    const bool valid = r < M;
-    const bool isc = valid && ch[r];
-    const int32_t cr = valid ? c[r] : -1;
-    int32_t tk, tc;
-    const int32_t kx = block_exclusive_scan<256>((int32_t)isc, 0, OpAdd(), lds, &tk) + ck;
-    int32_t cx = block_exclusive_scan<256>(isc ? cr : -1, -1, OpMax(), lds, &tc);
-    cx = max(cx, cc);
-    if (valid) posA[a + r] = isc ? (r + cr - kx) : (r + cx + 1 - kx);
-    ck += tk;
-    cc = max(cc, tc);
-  }
-  // columns, forward: Kc
-  ck = 0;
-  for (int32_t b = 0; b < M; b += 256) {
-    const int32_t j = b + threadIdx.x;
-    const bool valid = j < M;
-    const bool isc = valid && ch[iv[j]];
-    int32_t tk;
-    const int32_t kx = block_exclusive_scan<256>((int32_t)isc, 0, OpAdd(), lds, &tk) + ck;
-    if (valid) posR[a + j] = -kx;
-    ck += tk;
-  }
-  __syncthreads();
-  // columns, backward: rnext = min chain row among columns > j
-  int32_t cm = M;
-  const int32_t nb = (M + 255) / 256;
-  for (int32_t bb = nb - 1; bb >= 0; bb--) {
-    const int32_t jj = bb * 256 + (255 - threadIdx.x);  // reversed within tile
-    const bool valid = jj < M && jj >= 0;
-    const int32_t row = valid ? iv[jj] : 0;
-    const bool isc = valid && ch[row];
-    int32_t tm;
-    int32_t mx = block_exclusive_scan<256>(isc ? -row : -M, -M, OpMax(), lds, &tm);  // max of -row = -min row
-    int32_t rnext = min(-mx, cm);
-    if (valid) posR[a + jj] = rnext + jj + posR[a + jj];
-    cm = min(cm, -tm);
-  }
-  __syncthreads();
-  // scatter the sequence
   uint32_t* sq = seq + 2 * a;
-  for (int32_t r = threadIdx.x; r < M; r += 256) {
-    if (ch[r]) {
-      sq[posA[a + r]] = kIgn;
-    } else {
-      const int32_t x = c[r];
-      sq[posA[a + r]] = ((uint32_t)posR[a + x] << 2) | kAdd;
+  int32_t ck = 0, cc = -1;
+  for (int32_t b = 0; b < M; b += 1024) {
+    const int32_t r0 = b + 4 * threadIdx.x;
+    int32_t cv[4];
+    bool isc[4];
+    int2 v = make_int2(0, INT32_MIN);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const bool ok = r0 + q < M;
+      cv[q] = ok ? c[r0 + q] : 0;
+      isc[q] = ok && ch[r0 + q];
+      if (isc[q]) {
+        v.x++;
+        v.y = cv[q];
+      }
     }
-  }
-  for (int32_t j = threadIdx.x; j < M; j += 256) {
-    const int32_t row = iv[j];
-    if (!ch[row]) sq[posR[a + j]] = ((uint32_t)posA[a + row] << 2) | kRem;
-  }
-  __syncthreads();
-  // pair index of every second occurrence (pairs are emitted in second-occurrence order)
-  const int32_t L = 2 * u.P + u.K;
-  int32_t carry = 0;
-  for (int32_t b = 0; b < L; b += 256) {
-    const int32_t q = b + threadIdx.x;
-    bool second = false;
-    if (q < L) {
-      const uint32_t e = sq[q];
-      second = (e & 3) != kIgn && (int32_t)(e >> 2) < q;
+    int2 tot;
+    const int2 ex = block_scan_cnt_max(v, lds, &tot);
+    int32_t kx = ck + ex.x, cx = max(cc, ex.y);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int32_t r = r0 + q;
+      if (r < M) {
+        if (isc[q]) {
+          const int32_t pa = r + cv[q] - kx;
+          posA[a + r] = pa;
+          crow[a + kx] = r;
+          sq[pa] = kIgn;
+          kx++;
+          cx = cv[q];
+        } else {
+          posA[a + r] = r + cx + 1 - kx;
+        }
+      }
     }
-    int32_t t;
-    const int32_t ex = block_exclusive_scan<256>((int32_t)second, 0, OpAdd(), lds, &t);
-    if (second) sidx[2 * a + q] = carry + ex;
-    carry += t;
+    ck += tot.x;
+    cc = max(cc, tot.y);
   }
 }
 
-// Delta of each off-chain id (convert_to_diff_binary, :358-396): entries strictly
-// between its two occurrences that are in the decoder's list when it moves: IGNOREs,
-// REMOVEs whose element is still pending (its ADD comes later), ADDs whose element has
-// already been moved (its REMOVE came earlier).  Negative when the second occurrence is
-// the REMOVE.
-__global__ void __launch_bounds__(256) k_deltas(const Unit* __restrict__ units, const int32_t* __restrict__ cord,
-                                                const uint8_t* __restrict__ chain, const int32_t* __restrict__ posA,
-                                                const int32_t* __restrict__ posR, const uint32_t* __restrict__ seq,
-                                                const int32_t* __restrict__ sidx, int32_t* __restrict__ pid,
+// Columns pass: Kc = #chain columns before j; the REMOVE of off-chain column j sits at
+// rnext(j) + j - Kc with rnext = row of the Kc-th chain node (M past the last).  Writes both
+// entries of every off-chain element x = j: seq = partner position << 2 | type, sx = x.
+__global__ void __launch_bounds__(256) k_pos_cols(const Unit* __restrict__ units, const int32_t* __restrict__ inv,
+                                                  const uint8_t* __restrict__ chain, const int32_t* __restrict__ posA,
+                                                  const int32_t* __restrict__ crow, uint32_t* __restrict__ seq,
+                                                  int32_t* __restrict__ sx) {
+  __shared__ int32_t lds[4];
+  const Unit u = units[blockIdx.x];
+  const int64_t a = u.a;
+  const int32_t M = u.M, K = u.K;
+  uint32_t* sq = seq + 2 * a;
+  int32_t* sxa = sx + 2 * a;
+  int32_t ck = 0;
+  for (int32_t b = 0; b < M; b += 1024) {
+    const int32_t j0 = b + 4 * threadIdx.x;
+    int32_t row[4];
+    bool isc[4];
+    int32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const bool ok = j0 + q < M;
+      row[q] = ok ? inv[a + j0 + q] : 0;
+      isc[q] = !ok || chain[a + row[q]];
+      v += (ok && isc[q]) ? 1 : 0;
+    }
+    int32_t tot;
+    int32_t kc = ck + block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int32_t j = j0 + q;
+      if (isc[q]) {
+        kc++;
+        continue;
+      }
+      const int32_t pr = ((kc < K) ? crow[a + kc] : M) + j - kc;
+      const int32_t pa = posA[a + row[q]];
+      sq[pr] = ((uint32_t)pa << 2) | kRem;
+      sxa[pr] = j;
+      sq[pa] = ((uint32_t)pr << 2) | kAdd;
+      sxa[pa] = j;
+    }
+    ck += tot;
+  }
+}
+
+// Delta of each off-chain id (convert_to_diff_binary, :358-396), in second-occurrence order
+// (the pair order): entries strictly between its two occurrences that are in the decoder's
+// list when it moves -- IGNOREs, REMOVEs whose element is still pending (its ADD comes
+// later), ADDs whose element has already moved (its REMOVE came earlier).  Negative when the
+// second occurrence is the REMOVE.  The pair index is a running count of second occurrences.
+__global__ void __launch_bounds__(256) k_deltas(const Unit* __restrict__ units, const uint32_t* __restrict__ seq,
+                                                const int32_t* __restrict__ sx, int32_t* __restrict__ pid,
                                                 int32_t* __restrict__ pdl) {
+  __shared__ int32_t lds[4];
   const Unit u = units[blockIdx.x];
   const int64_t a = u.a;
   const uint32_t* sq = seq + 2 * a;
-  for (int32_t r = threadIdx.x; r < u.M; r += 256) {
-    if (chain[a + r]) continue;
-    const int32_t x = cord[a + r];
-    const int32_t pa = posA[a + r], pr = posR[a + x];
-    const int32_t f = min(pa, pr), s = max(pa, pr);
-    int32_t d = 0;
-    for (int32_t q = f + 1; q < s; q++) {
-      const uint32_t e = sq[q];
-      const uint32_t ty = e & 3;
-      const int32_t pt = (int32_t)(e >> 2);
-      d += (ty == kIgn) | ((ty == kRem) & (pt > s)) | ((ty == kAdd) & (pt < s));
+  const int32_t L = 2 * u.P + u.K;
+  int32_t ck = 0;
+  for (int32_t b = 0; b < L; b += 1024) {
+    const int32_t q0 = b + 4 * threadIdx.x;
+    uint32_t e[4];
+    int32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      e[q] = (q0 + q < L) ? sq[q0 + q] : kIgn;
+      if ((e[q] & 3) != kIgn && (int32_t)(e[q] >> 2) < q0 + q) v++;
     }
-    const int32_t k = sidx[2 * a + s];
-    pid[a + k] = x;
-    pdl[a + k] = (pr > pa) ? -d : d;
+    int32_t tot;
+    int32_t k = ck + block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int32_t s = q0 + q;
+      const uint32_t ty = e[q] & 3;
+      const int32_t f = (int32_t)(e[q] >> 2);
+      if (ty == kIgn || f >= s) continue;
+      int32_t d = 0;
+      for (int32_t z = f + 1; z < s; z++) {
+        const uint32_t y = sq[z];
+        const uint32_t yt = y & 3;
+        const int32_t pt = (int32_t)(y >> 2);
+        d += (yt == kIgn) | ((yt == kRem) & (pt > s)) | ((yt == kAdd) & (pt < s));
+      }
+      pid[a + k] = sx[2 * a + s];
+      pdl[a + k] = (ty == kRem) ? -d : d;
+      k++;
+    }
+    ck += tot;
   }
 }
 
