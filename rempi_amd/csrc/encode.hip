@@ -702,10 +702,14 @@ __global__ void __launch_bounds__(256) k_deltas(const Unit* __restrict__ units, 
                                                 const int32_t* __restrict__ sx, int32_t* __restrict__ pid,
                                                 int32_t* __restrict__ pdl) {
   __shared__ int32_t lds[4];
+  __shared__ int4 items[1024];  // second occurrences of the round: {position s, entry, id}
+  constexpr int32_t RING = 4096;  // the last RING sequence entries, for the span counts
+  __shared__ uint32_t ring[RING];
   const Unit u = units[blockIdx.x];
   const int64_t a = u.a;
   const uint32_t* sq = seq + 2 * a;
   const int32_t L = 2 * u.P + u.K;
+  const int g = threadIdx.x >> 4, j = threadIdx.x & 15, gw = (threadIdx.x >> 4) & 3;
   int32_t ck = 0;
   for (int32_t b = 0; b < L; b += 1024) {
     const int32_t q0 = b + 4 * threadIdx.x;
@@ -717,25 +721,38 @@ __global__ void __launch_bounds__(256) k_deltas(const Unit* __restrict__ units, 
       if ((e[q] & 3) != kIgn && (int32_t)(e[q] >> 2) < q0 + q) v++;
     }
     int32_t tot;
-    int32_t k = ck + block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);
+    int32_t k = block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const int32_t s = q0 + q;
-      const uint32_t ty = e[q] & 3;
-      const int32_t f = (int32_t)(e[q] >> 2);
-      if (ty == kIgn || f >= s) continue;
+      ring[(q0 + q) & (RING - 1)] = e[q];
+      if ((e[q] & 3) != kIgn && (int32_t)(e[q] >> 2) < q0 + q)
+        items[k++] = make_int4(q0 + q, (int32_t)e[q], sx[2 * a + q0 + q], 0);
+    }
+    __syncthreads();
+    const int32_t rlo = b + 1024 - RING;  // entries >= rlo are in the ring
+    // one item per 16-lane group: the group counts its span 16 entries at a time
+    for (int32_t it = g; it < tot; it += 16) {
+      const int4 item = items[it];
+      const int32_t s = item.x, f = (int32_t)((uint32_t)item.y >> 2);
       int32_t d = 0;
-      for (int32_t z = f + 1; z < s; z++) {
-        const uint32_t y = sq[z];
-        const uint32_t yt = y & 3;
-        const int32_t pt = (int32_t)(y >> 2);
-        d += (yt == kIgn) | ((yt == kRem) & (pt > s)) | ((yt == kAdd) & (pt < s));
+      for (int32_t z0 = f + 1; z0 < s; z0 += 16) {
+        const int32_t z = z0 + j;
+        bool c = false;
+        if (z < s) {
+          const uint32_t y = (z >= rlo) ? ring[z & (RING - 1)] : sq[z];
+          const uint32_t yt = y & 3;
+          const int32_t pt = (int32_t)(y >> 2);
+          c = (yt == kIgn) | ((yt == kRem) & (pt > s)) | ((yt == kAdd) & (pt < s));
+        }
+        d += __popc((uint32_t)(__ballot(c) >> (16 * gw)) & 0xFFFFu);
       }
-      pid[a + k] = sx[2 * a + s];
-      pdl[a + k] = (ty == kRem) ? -d : d;
-      k++;
+      if (j == 0) {
+        pid[a + ck + it] = item.z;
+        pdl[a + ck + it] = (((uint32_t)item.y & 3) == kRem) ? -d : d;
+      }
     }
     ck += tot;
+    __syncthreads();
   }
 }
 
