@@ -418,30 +418,98 @@ __global__ void __launch_bounds__(256) k_rank_tiles(const Unit* __restrict__ uni
                                                     const int32_t* __restrict__ lrank, const uint64_t* __restrict__ tminmax,
                                                     int32_t* __restrict__ cord, int32_t* __restrict__ inv,
                                                     uint64_t* __restrict__ skey) {
+  // Tile-level pruning first: tiles wholly below every key of this tile add their length,
+  // tiles wholly above add nothing, and only the overlapping ones (for near-sorted traces
+  // the neighbours) are binary-searched per key.
+  constexpr int kMaxOv = 64;
+  __shared__ int32_t ov[kMaxOv];
+  __shared__ int32_t nov, below;
   const SortTile w = st[blockIdx.x];
   const Unit u = units[w.unit];
   const int nt = (u.M + kSortTile - 1) / kSortTile;
-  const uint64_t* mm = tminmax + 2 * (int64_t)u.sort_tile0;  // {min,max} per tile, L1-resident
+  const uint64_t* mm = tminmax + 2 * (int64_t)u.sort_tile0;
   const int len = min(kSortTile, u.M - w.tile * kSortTile);
+  const uint64_t wmin = mm[2 * w.tile], wmax = mm[2 * w.tile + 1];
+  if (threadIdx.x == 0) {
+    nov = 0;
+    below = 0;
+  }
+  __syncthreads();
+  int32_t my_below = 0;
+  for (int q = threadIdx.x; q < nt; q += 256) {
+    if (q == w.tile) continue;
+    const int qlen = min(kSortTile, u.M - q * kSortTile);
+    const uint64_t qmin = mm[2 * q], qmax = mm[2 * q + 1];
+    // q < w counts keys <= x (equal keys of earlier rows first), q > w keys < x
+    const bool all = (q < w.tile) ? (qmax <= wmin) : (qmax < wmin);
+    const bool none = (q < w.tile) ? (qmin > wmax) : (qmin >= wmax);
+    if (all) my_below += qlen;
+    else if (!none) {
+      const int k = atomicAdd(&nov, 1);
+      if (k < kMaxOv) ov[k] = q;
+    }
+  }
+  my_below = wave_reduce(my_below, OpAdd());
+  if (lane_id() == 0 && my_below) atomicAdd(&below, my_below);
+  __syncthreads();
+  const int n_ov = nov;
+  const int32_t base = below;
+  // the (usually two) overlapping neighbour tiles are searched in LDS
+  constexpr int kLdsTiles = 2;
+  __shared__ uint64_t nk[kLdsTiles][kSortTile];
+  if (n_ov <= kLdsTiles) {
+    for (int k = 0; k < n_ov; k++) {
+      const int q = ov[k];
+      const int qlen = min(kSortTile, u.M - q * kSortTile);
+      for (int t = threadIdx.x; t < qlen; t += 256) nk[k][t] = tkey[u.a + (int64_t)q * kSortTile + t];
+    }
+    __syncthreads();
+  }
   for (int j = threadIdx.x; j < len; j += 256) {
     const int32_t i = w.tile * kSortTile + j;
     const uint64_t x = mkey[u.a + i];
-    int32_t rank = lrank[u.a + i];
-    for (int q = 0; q < nt; q++) {
-      if (q == w.tile) continue;
-      const int qlen = min(kSortTile, u.M - q * kSortTile);
-      const uint64_t* tk = tkey + u.a + (int64_t)q * kSortTile;
-      if (q < w.tile) {  // count keys <= x (equal keys from earlier rows come first)
-        if (mm[2 * q + 1] <= x) { rank += qlen; continue; }
-        if (mm[2 * q] > x) continue;
+    int32_t rank = lrank[u.a + i] + base;
+    if (n_ov <= kLdsTiles) {
+      for (int k = 0; k < n_ov; k++) {
+        const int q = ov[k];
+        const int qlen = min(kSortTile, u.M - q * kSortTile);
+        const uint64_t* tk = nk[k];
         int lo = 0, hi = qlen;
-        while (lo < hi) { int mid = (lo + hi) >> 1; if (tk[mid] <= x) lo = mid + 1; else hi = mid; }
+        if (q < w.tile) {
+          while (lo < hi) { const int mid = (lo + hi) >> 1; if (tk[mid] <= x) lo = mid + 1; else hi = mid; }
+        } else {
+          while (lo < hi) { const int mid = (lo + hi) >> 1; if (tk[mid] < x) lo = mid + 1; else hi = mid; }
+        }
         rank += lo;
-      } else {  // count keys < x
-        if (mm[2 * q + 1] < x) { rank += qlen; continue; }
-        if (mm[2 * q] >= x) continue;
+      }
+    } else if (n_ov <= kMaxOv) {
+      for (int k = 0; k < n_ov; k++) {
+        const int q = ov[k];
+        const int qlen = min(kSortTile, u.M - q * kSortTile);
+        const uint64_t* tk = tkey + u.a + (int64_t)q * kSortTile;
         int lo = 0, hi = qlen;
-        while (lo < hi) { int mid = (lo + hi) >> 1; if (tk[mid] < x) lo = mid + 1; else hi = mid; }
+        if (q < w.tile) {
+          while (lo < hi) { const int mid = (lo + hi) >> 1; if (tk[mid] <= x) lo = mid + 1; else hi = mid; }
+        } else {
+          while (lo < hi) { const int mid = (lo + hi) >> 1; if (tk[mid] < x) lo = mid + 1; else hi = mid; }
+        }
+        rank += lo;
+      }
+    } else {  // many overlapping tiles (e.g. a reversed or random permutation): test them all
+      for (int q = 0; q < nt; q++) {
+        if (q == w.tile) continue;
+        const int qlen = min(kSortTile, u.M - q * kSortTile);
+        const uint64_t qmin = mm[2 * q], qmax = mm[2 * q + 1];
+        const bool all = (q < w.tile) ? (qmax <= wmin) : (qmax < wmin);
+        const bool none = (q < w.tile) ? (qmin > wmax) : (qmin >= wmax);
+        if (all || none) continue;  // already in base / contributes nothing
+        const uint64_t* tk = tkey + u.a + (int64_t)q * kSortTile;
+        int lo = 0, hi = qlen;
+        if (q < w.tile) {
+          while (lo < hi) { const int mid = (lo + hi) >> 1; if (tk[mid] <= x) lo = mid + 1; else hi = mid; }
+        } else {
+          while (lo < hi) { const int mid = (lo + hi) >> 1; if (tk[mid] < x) lo = mid + 1; else hi = mid; }
+        }
         rank += lo;
       }
     }
