@@ -613,7 +613,7 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
     std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return units[a].P > units[b].P; });
     int32_t* d_order = c->upload("d_perm_order", order, s);
     c->launch(K_DEC_WIN1, k_dec_perm_grp, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order, NU, d_in,
-              d_idd, d_dld, d_perm, d_cinv, d_nfail);
+              d_idd, d_dld, d_perm, d_cinv, d_nfail, getenv("CDCX_XMODE") ? atoi(getenv("CDCX_XMODE")) : 0);
   }
   int32_t nf = c->dec_tier > 0 ? NU : c->download(d_nfail, 1, s)[0];
   if (nf > 0) {

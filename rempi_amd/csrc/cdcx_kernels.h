@@ -75,7 +75,7 @@ __global__ void k_dec_sections(const DUnit*, const uint8_t*, uint64_t*, uint64_t
 __global__ void k_dec_perm_lane(const DUnit*, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*, int32_t*,
                                 uint32_t*);
 __global__ void k_dec_perm_grp(DUnit*, const int32_t*, int32_t, const uint8_t*, uint64_t*, uint64_t*, int32_t*, int32_t*,
-                               int32_t*);
+                               int32_t*, int32_t);
 __global__ void k_dec_cinv(const DUnit*, const int32_t*, int32_t*);
 template <int K>
 __global__ void k_dec_perm_window(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);

@@ -444,10 +444,10 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
                                                      int32_t n_units, const uint8_t* __restrict__ in,
                                                      uint64_t* __restrict__ idd, uint64_t* __restrict__ dld,
                                                      int32_t* __restrict__ perm, int32_t* __restrict__ cinv,
-                                                     int32_t* __restrict__ nfail) {
+                                                     int32_t* __restrict__ nfail, int32_t xmode) {
   constexpr int32_t W = kGW, WM = kGW - 1, MM = kGMap - 1;
-  __shared__ int32_t win_all[4][W];
-  __shared__ int2 emap_all[4][kGMap];  // {element, absolute position}
+  __shared__ int32_t win_all[4][W + 16];      // + one dummy slot per lane
+  __shared__ int2 emap_all[4][kGMap + 16];    // {element, absolute position}; + dummies
   const int g = threadIdx.x >> 4, j = threadIdx.x & 15;
   int32_t* win = win_all[g];
   int2* emap = emap_all[g];
@@ -475,27 +475,81 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
   for (int32_t q = j; q < W; q += 16) win[q] = q;
   for (int32_t q = j; q < kGMap; q += 16) emap[q] = (q < W) ? make_int2(q, q) : make_int2(-1, -1);
   int32_t base = 0;
-  bool fail = !sim;
+  int32_t failv = sim ? 0 : 1;
   const int32_t Pmax = __builtin_amdgcn_readfirstlane(wave_reduce(P, OpMax()));
   auto slide = [&](bool go) {  // settle [base, base+16), open [base+W, base+W+16) as identity
-    if (go) {
-      const int32_t ph = (base + j) & WM;
-      const int32_t v = win[ph];
-      if (v < M) {
-        pm[v] = base + j;
-        ci[base + j] = v;
-      }
-      const int32_t e = base + W + j;
-      win[ph] = e;
-      emap[e & MM] = make_int2(e, e);
-      base += 16;
+    const int32_t ph = go ? ((base + j) & WM) : W + j;
+    const int32_t v = win[ph];  // (dummy slot when not sliding)
+    if (go && v < M && !(xmode & 2)) {
+      pm[v] = base + j;
+      ci[base + j] = v;
     }
+    const int32_t e = base + W + j;
+    __builtin_amdgcn_wave_barrier();
+    win[ph] = e;
+    emap[go ? (e & MM) : kGMap + j] = make_int2(e, e);
+    if (go) base += 16;
   };
-  for (int32_t k0 = 0; k0 < Pmax; k0 += 16) {
-    // inverse LP of the next 16 pairs: x = prefix(prefix(y)) of the sign-extended int32
-    // sections, mod 2^64 (decode :1004-1014 + :157-168); the sim uses the low 32 bits
+  // one pair of all four groups: x, d group-uniform
+  auto step = [&](int32_t k, int32_t x, int32_t d) {
+      // Common path without divergent branches: predicated selects, LDS accesses of
+      // inactive lanes go to per-lane dummy slots; rare cases (slides, targets past the
+      // window, rotations longer than 16 slots) take wave-uniform detours.
+      const int32_t live = (k < P) ? 1 : 0;
+      const int32_t xbad = live & ((uint32_t)x >= (uint32_t)M ? 1 : 0);
+      failv |= xbad;
+      int32_t act = live & (failv ^ 1);
+      // an untouched x (at position x) is brought kGAhead slots before the window end
+      const int32_t far = act & (x >= base + W ? 1 : 0);
+      if (__builtin_amdgcn_ballot_w64(far))
+        while (__builtin_amdgcn_ballot_w64(far && x >= base + W - kGAhead)) slide(far && x >= base + W - kGAhead);
+      const int2 e = emap[act ? (x & MM) : kGMap + j];
+      int32_t p = e.y - base;
+      int32_t t = p + d;
+      const int32_t bad = act & ((e.x != x) | ((uint32_t)p >= (uint32_t)W) | (t < 0) | (base + t > M - 1) ? 1 : 0);
+      failv |= bad;
+      act &= bad ^ 1;
+      if (__builtin_amdgcn_ballot_w64(act && t > W - 1)) {
+        while (__builtin_amdgcn_ballot_w64(act && t > W - 1)) {
+          const int32_t go = act & (t > W - 1 ? 1 : 0);
+          const int32_t stuck = go & (p < 16 ? 1 : 0);
+          failv |= stuck;
+          act &= stuck ^ 1;
+          const int32_t sl = go & (stuck ^ 1);
+          slide(sl != 0);
+          p -= 16 * sl;
+          t -= 16 * sl;
+        }
+      }
+      // rotation of the slots between p and t, 16 at a time
+      const bool fwd = t >= p;
+      const int32_t len = fwd ? t - p : p - t;
+      const int32_t dir = fwd ? 1 : -1;
+      auto chunk = [&](int32_t c) {
+        const int32_t o = c + j;
+        const bool sel = act && o <= len;
+        const int32_t s = p + dir * o;
+        const int32_t rd = (sel && o < len) ? ((base + s + dir) & WM) : W + j;
+        int32_t w = win[rd];
+        asm volatile("" : "+v"(w));  // keep the read unconditional (no exec-mask branch around it)
+        const int32_t v = (o < len) ? w : x;
+        __builtin_amdgcn_wave_barrier();
+        win[sel ? ((base + s) & WM) : W + j] = v;
+        emap[sel ? (v & MM) : kGMap + j] = make_int2(v, base + s);
+        __builtin_amdgcn_wave_barrier();
+      };
+      if (!(xmode & 1)) chunk(0);
+      if (!(xmode & 1) && __builtin_amdgcn_ballot_w64(act && len >= 16))
+        for (int32_t c = 16; __builtin_amdgcn_ballot_w64(act && c <= len); c += 16) chunk(c);
+  };
+  // 16 pairs at a time: inverse LP of the raw words (x = prefix(prefix(y)) of the
+  // sign-extended int32 sections, mod 2^64, decode :1004-1014 + :157-168; the sim uses the
+  // low 32 bits), then the steps, each taking group lane 0 (row_newbcast:0) and shifting
+  // the batch down a lane
+  int32_t xs = 0, ds = 0;
+  auto lp = [&](int32_t k0, int32_t yw_i, int32_t yw_d) {
     const bool inb = k0 + j < P;
-    const int64_t yi = inb ? (int64_t)yid[k0 + j] : 0, yd = inb ? (int64_t)ydl[k0 + j] : 0;
+    const int64_t yi = (xmode & 8) ? (k0 + j == 0 ? 1 : 0) : (int64_t)yw_i, yd = (xmode & 8) ? 0 : (int64_t)yw_d;
     const int64_t zi = row_incl_scan64(yi), zd = row_incl_scan64(yd);
     const int64_t xi = cxi + (int64_t)(j + 1) * czi + row_incl_scan64(zi);
     const int64_t xd = cxd + (int64_t)(j + 1) * czd + row_incl_scan64(zd);
@@ -503,53 +557,40 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
     czd += __shfl(zd, 15, 16);
     cxi = __shfl(xi, 15, 16);
     cxd = __shfl(xd, 15, 16);
-    if (inb) {
+    if (inb && !(xmode & 4)) {
       ip[k0 + j] = (uint64_t)xi;
       dp[k0 + j] = (uint64_t)xd;
     }
-    const int32_t xv = (int32_t)xi, dv = (int32_t)xd;
-    static_for<16>([&](auto qc) {
-      constexpr int q = decltype(qc)::value;
-      if (k0 + q >= Pmax) return;
-      const int32_t x = row_bcast<q>(xv);
-      const int32_t d = row_bcast<q>(dv);
-      bool act = !fail && (k0 + q < P);
-      if (act && (uint32_t)x >= (uint32_t)M) { fail = true; act = false; }
-      // untouched x (at position x): slide until it is kGAhead slots before the window end
-      const bool far = act && x >= base + W;
-      while (__builtin_amdgcn_ballot_w64(far && x >= base + W - kGAhead)) slide(far && x >= base + W - kGAhead);
-      int2 e = make_int2(-1, -1);
-      if (act) e = emap[x & MM];
-      int32_t p = e.y - base;
-      if (act && (e.x != x || (uint32_t)p >= (uint32_t)W)) { fail = true; act = false; }
-      int32_t t = p + d;
-      if (act && (t < 0 || base + t > M - 1)) { fail = true; act = false; }
-      while (__builtin_amdgcn_ballot_w64(act && t > W - 1)) {
-        const bool go = act && t > W - 1;
-        if (go && p < 16) { fail = true; act = false; }
-        const bool sl = go && act;
-        slide(sl);
-        if (sl) {
-          p -= 16;
-          t -= 16;
-        }
-      }
-      // rotation of the slots between p and t
-      const bool fwd = t >= p;
-      const int32_t len = fwd ? t - p : p - t;
-      for (int32_t c = 0; __builtin_amdgcn_ballot_w64(act && c <= len); c += 16) {
-        const int32_t o = c + j;
-        if (act && o <= len) {
-          const int32_t s = fwd ? p + o : p - o;
-          const int32_t v = (o < len) ? win[(base + s + (fwd ? 1 : -1)) & WM] : x;
-          __builtin_amdgcn_wave_barrier();
-          win[(base + s) & WM] = v;
-          emap[v & MM] = make_int2(v, base + s);
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-    });
+    xs = (int32_t)xi;
+    ds = (int32_t)xd;
+  };
+  auto steps = [&](int32_t k0) {
+    const int32_t nq = min(16, Pmax - k0);
+    for (int32_t q = 0; q < nq; q++) {
+      const int32_t x = row_bcast<0>(xs), d = row_bcast<0>(ds);
+      xs = __builtin_amdgcn_update_dpp(xs, xs, 0x101, 0xf, 0xf, false);  // row_shl:1
+      ds = __builtin_amdgcn_update_dpp(ds, ds, 0x101, 0xf, 0xf, false);
+      step(k0 + q, x, d);
+    }
+  };
+  // Two batches per round.  The raw words of a batch are loaded one batch ahead, and each
+  // load is issued only after the previous wait (the compiler waits for all outstanding
+  // memory operations at every use), so a wait never covers a load issued just before it.
+  auto ld = [&](const int32_t* y, int32_t k) { return (k + j < P) ? y[k + j] : 0; };
+  int32_t ai = ld(yid, 0), ad = ld(ydl, 0), bi = ld(yid, 16), bd = ld(ydl, 16);
+  for (int32_t k0 = 0; k0 < Pmax; k0 += 32) {
+    lp(k0, ai, ad);
+    ai = ld(yid, k0 + 32);
+    ad = ld(ydl, k0 + 32);
+    steps(k0);
+    if (k0 + 16 < Pmax) {
+      lp(k0 + 16, bi, bd);
+      bi = ld(yid, k0 + 48);
+      bd = ld(ydl, k0 + 48);
+      steps(k0 + 16);
+    }
   }
+  const bool fail = failv != 0;
   if (sim && fail && j == 0) {
     units[ui].fb = 1;
     atomicAdd(nfail, 1);
