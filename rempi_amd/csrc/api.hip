@@ -254,7 +254,6 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int16_t* d_dense = c->buf<int16_t>("dense", (size_t)R * kMaxSets);
   int32_t* d_setlist = c->buf<int32_t>("setlist", (size_t)R * kMaxSets);
   int32_t* d_nsets = c->buf<int32_t>("nsets", R);
-  uint8_t* d_tix = c->buf<uint8_t>("tix", N);
   uint32_t* d_hist = c->buf<uint32_t>("hist", NT * kMaxSets);
   int32_t* d_base = c->buf<int32_t>("base", NT * kMaxSets);
   int32_t* d_tstart = c->buf<int32_t>("tstart", (size_t)R * (kMaxSets + 1));
@@ -272,13 +271,12 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int2* d_chunk_cap = c->buf<int2>("chunk_cap", ccap_off[R]);
   int32_t* d_nchunks = c->buf<int32_t>("nchunks", R);
 
-  c->launch(K_SET_PRESENCE, k_set_presence, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, d_presence, d_err);
+  c->launch(K_TILE_HIST, k_tile_hist, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, d_hist, d_presence, d_err);
   c->launch(K_SET_DENSE, k_set_dense, dim3(R), dim3(kMaxSets), s, (const uint32_t*)d_presence, d_dense, d_setlist, d_nsets);
-  c->launch(K_TILE_HIST, k_tile_hist, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, (const int16_t*)d_dense, d_tix,
-            d_hist);
   c->launch(K_HIST_SCAN, k_hist_scan, dim3(R), dim3(256), s, (const uint32_t*)d_hist, (const int32_t*)d_tile0,
-            (const int32_t*)d_ntiles, (const int32_t*)d_nsets, (const int64_t*)d_rec_off, d_base, d_tstart, d_tfirst);
-  c->launch(K_SCATTER, k_scatter, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, (const uint8_t*)d_tix,
+            (const int32_t*)d_ntiles, (const int32_t*)d_nsets, (const int32_t*)d_setlist, (const int64_t*)d_rec_off, d_base,
+            d_tstart, d_tfirst);
+  c->launch(K_SCATTER, k_scatter, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, (const int16_t*)d_dense,
             (const int32_t*)d_base, (const int64_t*)d_rec_off, d_trec, d_t2s);
   c->launch(K_INC0, k_inc0, dim3(NT), dim3(256), s, (const TRec*)d_trec, (const int32_t*)d_t2s, (const uint8_t*)d_tfirst,
             (const Tile*)d_tiles, (const int64_t*)d_rec_off, d_inc0);
@@ -392,9 +390,9 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int32_t* d_seghist = c->buf<int32_t>("seghist", 4096);
   int32_t* d_segord = c->buf<int32_t>("segord", nsegs);
   HIPCHK(hipMemsetAsync(d_seghist, 0, 4096 * 4, s));
-  c->launch(K_SEG_SORT, k_seg_hist, dim3(blocks(nsegs, 256)), dim3(256), s, (const Seg*)d_segs, (int32_t)nsegs, d_seghist);
+  c->launch(K_SEG_SORT, k_seg_hist, dim3(blocks(nsegs, 1024)), dim3(256), s, (const Seg*)d_segs, (int32_t)nsegs, d_seghist);
   c->launch(K_SEG_SORT, k_seg_bins, dim3(1), dim3(256), s, d_seghist);
-  c->launch(K_SEG_SORT, k_seg_order, dim3(blocks(nsegs, 256)), dim3(256), s, (const Seg*)d_segs, (int32_t)nsegs, d_seghist,
+  c->launch(K_SEG_SORT, k_seg_order, dim3(blocks(nsegs, 1024)), dim3(256), s, (const Seg*)d_segs, (int32_t)nsegs, d_seghist,
             d_segord);
   int32_t* d_par = c->buf<int32_t>("par", N);
   int32_t* d_exta = c->buf<int32_t>("exta", N);

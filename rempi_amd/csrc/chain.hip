@@ -65,14 +65,23 @@ __global__ void __launch_bounds__(256) k_seg_list(const Unit* __restrict__ units
   }
 }
 
-// Longest-first order of the segments (counting sort on the length, descending): blocks
-// take strided positions of this order so every block gets a similar amount of work, and a
-// wave's lanes run segments of similar length.
+// Longest-first order of the segments (counting sort on the length, descending; lengths
+// past kLenBins share the first bin): blocks take strided positions of this order so every
+// block gets a similar amount of work, and a wave's lanes run segments of similar length.
+// Counts are aggregated per block in LDS, so the global atomics are one per (block,
+// length present in the block).
 constexpr int kLenBins = 4096;
+__device__ __forceinline__ int len_bin(int32_t len) { return kLenBins - 1 - min(len, kLenBins - 1); }
 
 __global__ void __launch_bounds__(256) k_seg_hist(const Seg* __restrict__ segs, int32_t nsegs, int32_t* __restrict__ hist) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < nsegs) atomicAdd(&hist[kLenBins - 1 - min(segs[i].len, kLenBins - 1)], 1);
+  __shared__ int32_t h[kLenBins];
+  for (int q = threadIdx.x; q < kLenBins; q += 256) h[q] = 0;
+  __syncthreads();
+  for (int i = blockIdx.x * 1024 + threadIdx.x; i < min(nsegs, (int)(blockIdx.x + 1) * 1024); i += 256)
+    atomicAdd(&h[len_bin(segs[i].len)], 1);
+  __syncthreads();
+  for (int q = threadIdx.x; q < kLenBins; q += 256)
+    if (h[q]) atomicAdd(&hist[q], h[q]);
 }
 
 __global__ void __launch_bounds__(256) k_seg_bins(int32_t* __restrict__ hist) {
@@ -89,8 +98,30 @@ __global__ void __launch_bounds__(256) k_seg_bins(int32_t* __restrict__ hist) {
 
 __global__ void __launch_bounds__(256) k_seg_order(const Seg* __restrict__ segs, int32_t nsegs, int32_t* __restrict__ hist,
                                                    int32_t* __restrict__ order) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < nsegs) order[atomicAdd(&hist[kLenBins - 1 - min(segs[i].len, kLenBins - 1)], 1)] = i;
+  __shared__ int32_t h[kLenBins];
+  for (int q = threadIdx.x; q < kLenBins; q += 256) h[q] = 0;
+  __syncthreads();
+  const int i0 = blockIdx.x * 1024;
+  int bin[4], rk[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int i = i0 + q * 256 + threadIdx.x;
+    bin[q] = 0;
+    rk[q] = 0;
+    if (i < nsegs) {
+      bin[q] = len_bin(segs[i].len);
+      rk[q] = atomicAdd(&h[bin[q]], 1);
+    }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < kLenBins; q += 256)
+    if (h[q]) h[q] = atomicAdd(&hist[q], h[q]);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int i = i0 + q * 256 + threadIdx.x;
+    if (i < nsegs) order[h[bin[q]] + rk[q]] = i;
+  }
 }
 
 namespace {

@@ -17,20 +17,26 @@
 namespace cdcx {
 
 // ---------------------------------------------------------------------------------------
-// Set discovery: which matching_set_ids occur in each rank (limit: [0, kMaxSets)).
-__global__ void __launch_bounds__(256) k_set_presence(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
-                                                      uint32_t* __restrict__ presence, uint32_t* err) {
-  __shared__ uint32_t bm[kMaxSets / 32];
-  if (threadIdx.x < kMaxSets / 32) bm[threadIdx.x] = 0;
+// Set discovery + per-tile histograms in one pass over the records: hist[tile][set id]
+// and, per rank, which matching_set_ids occur (limit: [0, kMaxSets)).
+__global__ void __launch_bounds__(256) k_tile_hist(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
+                                                   uint32_t* __restrict__ hist, uint32_t* __restrict__ presence,
+                                                   uint32_t* err) {
+  __shared__ uint32_t h[kMaxSets];
+  h[threadIdx.x] = 0;
   __syncthreads();
   const Tile t = tiles[blockIdx.x];
   for (int i = threadIdx.x; i < t.len; i += blockDim.x) {
-    int32_t sid = rec[(t.start + i) * 8 + 7];
+    const int32_t sid = rec[(t.start + i) * 8 + 7];
     if ((uint32_t)sid >= (uint32_t)kMaxSets) raise_error(err, kErrLimit);
-    else atomicOr(&bm[sid >> 5], 1u << (sid & 31));
+    else atomicAdd(&h[sid], 1u);
   }
   __syncthreads();
-  if (threadIdx.x < kMaxSets / 32 && bm[threadIdx.x]) atomicOr(&presence[t.rank * (kMaxSets / 32) + threadIdx.x], bm[threadIdx.x]);
+  const uint32_t v = h[threadIdx.x];
+  hist[(int64_t)blockIdx.x * kMaxSets + threadIdx.x] = v;
+  const uint64_t nz = __ballot(v != 0);
+  if (lane_id() == 0 && (uint32_t)nz) atomicOr(&presence[t.rank * (kMaxSets / 32) + wave_id() * 2], (uint32_t)nz);
+  if (lane_id() == 32 && (uint32_t)(nz >> 32)) atomicOr(&presence[t.rank * (kMaxSets / 32) + wave_id() * 2 + 1], (uint32_t)(nz >> 32));
 }
 
 // Dense table index per (rank, set id): tables are numbered in ascending set id, which is
@@ -48,42 +54,26 @@ __global__ void __launch_bounds__(kMaxSets) k_set_dense(const uint32_t* __restri
   if (sid == kMaxSets - 1) nsets[r] = below + (here ? 1 : 0);
 }
 
-// Per-tile table histogram (and the dense table index of every record).
-__global__ void __launch_bounds__(256) k_tile_hist(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
-                                                   const int16_t* __restrict__ dense, uint8_t* __restrict__ tix,
-                                                   uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[kMaxSets];
-  h[threadIdx.x] = 0;
-  __syncthreads();
-  const Tile t = tiles[blockIdx.x];
-  for (int i = threadIdx.x; i < t.len; i += blockDim.x) {
-    int32_t sid = rec[(t.start + i) * 8 + 7];
-    int d = ((uint32_t)sid < (uint32_t)kMaxSets) ? dense[t.rank * kMaxSets + sid] : 0;
-    tix[t.start + i] = (uint8_t)d;
-    atomicAdd(&h[d], 1u);
-  }
-  __syncthreads();
-  hist[(int64_t)blockIdx.x * kMaxSets + threadIdx.x] = h[threadIdx.x];
-}
-
 // Per rank: exclusive scan of the tile histograms in (table, tile) order -> where each
 // tile's records of each table start in T-order; table starts; first-of-table flags.
 __global__ void __launch_bounds__(256) k_hist_scan(const uint32_t* __restrict__ hist, const int32_t* __restrict__ tile0,
                                                    const int32_t* __restrict__ ntiles, const int32_t* __restrict__ nsets,
-                                                   const int64_t* __restrict__ rec_off, int32_t* __restrict__ base,
-                                                   int32_t* __restrict__ tstart, uint8_t* __restrict__ tfirst) {
+                                                   const int32_t* __restrict__ setlist, const int64_t* __restrict__ rec_off,
+                                                   int32_t* __restrict__ base, int32_t* __restrict__ tstart,
+                                                   uint8_t* __restrict__ tfirst) {
   __shared__ int32_t lds[4];
   const int r = blockIdx.x;
   const int T = nsets[r], t0 = tile0[r], nt = ntiles[r];
   int32_t run = 0;
   for (int t = 0; t < T; t++) {
+    const int sid = setlist[r * kMaxSets + t];
     if (threadIdx.x == 0) {
       tstart[r * (kMaxSets + 1) + t] = run;
       tfirst[rec_off[r] + run] = 1;
     }
     for (int c = 0; c < nt; c += 256) {
       int i = c + threadIdx.x;
-      int32_t v = (i < nt) ? (int32_t)hist[(int64_t)(t0 + i) * kMaxSets + t] : 0;
+      int32_t v = (i < nt) ? (int32_t)hist[(int64_t)(t0 + i) * kMaxSets + sid] : 0;
       int32_t tot;
       int32_t ex = block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);
       if (i < nt) base[(int64_t)(t0 + i) * kMaxSets + t] = run + ex;
@@ -97,23 +87,37 @@ __global__ void __launch_bounds__(256) k_hist_scan(const uint32_t* __restrict__ 
 // wave, records with the same table find each other with 8 ballots (one per bit of the
 // table index), which keeps the partition stable for any number of tables.
 __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
-                                                 const uint8_t* __restrict__ tix, const int32_t* __restrict__ base,
+                                                 const int16_t* __restrict__ dense, const int32_t* __restrict__ base,
                                                  const int64_t* __restrict__ rec_off, TRec* __restrict__ trec,
                                                  int32_t* __restrict__ t2s) {
   constexpr int ROUNDS = kTile / 256;
   __shared__ int32_t wc[ROUNDS * 4 * kMaxSets];  // [round][wave][table]
   for (int i = threadIdx.x; i < ROUNDS * 4 * kMaxSets; i += 256) wc[i] = 0;
-  __syncthreads();
   const Tile t = tiles[blockIdx.x];
   const int w = wave_id(), l = lane_id();
   const uint64_t lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+  int4 lo[ROUNDS], hi[ROUNDS];
+#pragma unroll
+  for (int j = 0; j < ROUNDS; j++) {
+    const int i = j * 256 + threadIdx.x;
+    if (i < t.len) {
+      const int4* rp = reinterpret_cast<const int4*>(rec + (t.start + i) * 8);
+      lo[j] = rp[0];
+      hi[j] = rp[1];
+    } else {
+      lo[j] = make_int4(0, 0, 0, 0);
+      hi[j] = make_int4(0, 0, 0, 0);
+    }
+  }
+  __syncthreads();
   int my_t[ROUNDS];
   int my_rank[ROUNDS];
 #pragma unroll
   for (int j = 0; j < ROUNDS; j++) {
     const int i = j * 256 + threadIdx.x;
     const bool valid = i < t.len;
-    const int tb = valid ? tix[t.start + i] : 0;
+    const int32_t sid = hi[j].w;
+    const int tb = valid ? dense[t.rank * kMaxSets + ((uint32_t)sid < (uint32_t)kMaxSets ? sid : 0)] : 0;
     uint64_t peers = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < 8; b++) {
@@ -143,15 +147,13 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
     if (i >= t.len) continue;
     const int tb = my_t[j];
     const int32_t pos = base[(int64_t)blockIdx.x * kMaxSets + tb] + wc[(j * 4 + w) * kMaxSets + tb] + my_rank[j];
-    const int4* rp = reinterpret_cast<const int4*>(rec + (t.start + i) * 8);
-    const int4 lo = rp[0], hi = rp[1];
     // lo = {count, type, flag, rank}, hi = {with_next, index, clock, set}
     TRec o;
-    const bool matched = (lo.z == 1);
-    o.src = lo.w;
-    o.clk = hi.z;
-    o.x = matched ? hi.y : lo.x;
-    o.info = matched ? (0x80000000u | (hi.x != 0 ? 1u : 0u)) : 0u;
+    const bool matched = (lo[j].z == 1);
+    o.src = lo[j].w;
+    o.clk = hi[j].z;
+    o.x = matched ? hi[j].y : lo[j].x;
+    o.info = matched ? (0x80000000u | (hi[j].x != 0 ? 1u : 0u)) : 0u;
     trec[rb + pos] = o;
     t2s[rb + pos] = spos0 + i;
   }
@@ -320,49 +322,53 @@ __global__ void __launch_bounds__(256) k_unit_prep(Unit* __restrict__ units, con
                                                    uint64_t* __restrict__ mkey, int32_t* __restrict__ midx,
                                                    int32_t* __restrict__ wp, int32_t* __restrict__ run_id,
                                                    uint64_t* __restrict__ run_cnt, uint32_t* err) {
-  __shared__ int32_t lds[4];
+  // The three counts (matched, with_next, unmatched run starts) travel through one scan,
+  // packed into 21-bit fields.
+  __shared__ uint64_t lds[4];
   Unit& u = units[blockIdx.x];
   const int64_t a = u.a;
   const int32_t n = u.n;
   int32_t cm = 0, cw = 0, cr = 0;
+  constexpr uint64_t F = 1ull << 21;
   for (int32_t b = 0; b < n; b += 256) {
     const int32_t k = b + threadIdx.x;
     const bool valid = k < n;
-    TRec r = valid ? trec[a + k] : TRec{0, 0, 0, 0};
+    const TRec r = valid ? trec[a + k] : TRec{0, 0, 0, 0};
     const bool m = valid && (r.info >> 31);
     const bool wn = m && (r.info & 1);
-    bool rs = false;
-    if (valid && !m) rs = (k == 0) || (trec[a + k - 1].info >> 31);
-    int32_t tm, tw, tr;
-    const int32_t mo = block_exclusive_scan<256>((int32_t)m, 0, OpAdd(), lds, &tm);
-    const int32_t wo = block_exclusive_scan<256>((int32_t)wn, 0, OpAdd(), lds, &tw);
-    const int32_t ro = block_exclusive_scan<256>((int32_t)rs, 0, OpAdd(), lds, &tr);
+    const bool rs = valid && !m && ((k == 0) || (trec[a + k - 1].info >> 31));
+    uint64_t tot;
+    const uint64_t ex =
+        block_exclusive_scan<256>((uint64_t)m + (uint64_t)wn * F + (uint64_t)rs * F * F, (uint64_t)0, OpAdd(), lds, &tot);
+    const int32_t mo = cm + (int32_t)(ex & (F - 1));
     if (m) {
-      mkey[a + cm + mo] = pack_key(r.clk, r.src);
-      midx[a + cm + mo] = r.x;
+      mkey[a + mo] = pack_key(r.clk, r.src);
+      midx[a + mo] = r.x;
     }
-    if (wn) wp[a + cw + wo] = cm + mo;
-    if (rs) {
+    if (wn) wp[a + cw + (int32_t)((ex >> 21) & (F - 1))] = mo;
+    if (rs) {  // the run: this and the following unmatched records (add(), :205-208)
       uint64_t cnt = sext(r.x);
       for (int32_t j = k + 1; j < n; j++) {
-        TRec q = trec[a + j];
+        const TRec q = trec[a + j];
         if (q.info >> 31) break;
         cnt += sext(q.x);
       }
-      run_id[a + cr + ro] = cm + mo;
-      run_cnt[a + cr + ro] = cnt;
+      const int32_t ro = cr + (int32_t)(ex >> 42);
+      run_id[a + ro] = mo;
+      run_cnt[a + ro] = cnt;
     }
-    cm += tm;
-    cw += tw;
-    cr += tr;
+    cm += (int32_t)(tot & (F - 1));
+    cw += (int32_t)((tot >> 21) & (F - 1));
+    cr += (int32_t)(tot >> 42);
   }
   if (threadIdx.x == 0) {
     u.M = cm;
     u.U = cr;
     u.W = cw;
-    // A table must not end inside a with_next group (format(), :229-233).
-    if (cw > 0 && wp[a + cw - 1] == cm - 1) raise_error(err, kErrTruncated);
   }
+  // A table must not end inside a with_next group (format(), :229-233).
+  __syncthreads();
+  if (threadIdx.x == 0 && cw > 0 && wp[a + cw - 1] == cm - 1) raise_error(err, kErrTruncated);
 }
 
 // ---------------------------------------------------------------------------------------
