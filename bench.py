@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-sample-events", type=int, default=1_000_000)
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--kernel-report", action="store_true", help="print per-kernel times to stderr")
+    ap.add_argument("--streams", type=int, default=2, help="rank batches in flight per GPU (one HIP stream each)")
+    ap.add_argument("--host-io", type=int, default=1, help="steps of the copy-inclusive measurement (0 = skip)")
     return ap.parse_args()
 
 
@@ -126,6 +128,69 @@ def _port_one(a):
 
 
 # ---------------------------------------------------------------------------------------
+class Lane:
+    """One rank batch on its own HIP stream and context (the bench runs --streams of them
+    side by side, one host thread each, so one batch's latency-bound phases overlap the
+    other's bandwidth-bound ones)."""
+
+    def __init__(self, args, p, first, n, device):
+        import rempi_amd
+        from rempi_amd import cdcx
+
+        self.cdcx = cdcx
+        self.first, self.n = first, n
+        self.stream = cdcx.stream_create()
+        self.ctx = rempi_amd.Context(max_event_length=args.max_len, device=device)
+        self.d_rec, self.rec_off = self.ctx.generate_device(p, first, n, stream=self.stream)
+        cdcx.stream_sync(self.stream)
+        self.records = int(self.rec_off[-1])
+        self.comp = 0
+        self.n_out = 0
+
+    def step(self):
+        c = self.ctx
+        d_out, off, ln = c.encode_batch_device(self.d_rec, self.rec_off, stream=self.stream)
+        d_keys, n_keys = c.batch_sorted_keys()
+        _, n_out, _ = c.decode_batch_device(d_out, off, ln, d_keys, n_keys, stream=self.stream)
+        self.comp += int(ln.sum())
+        self.n_out = n_out
+        return d_out, off, ln
+
+    def host_io_step(self, pin_rec, pin_files, pin_recs):
+        """Copy-inclusive: records H2D from pinned host memory, encode + decode, rank files
+        and decoded records D2H into pinned host memory."""
+        cd, c, s = self.cdcx, self.ctx, self.stream
+        cd.memcpy_async(self.d_rec, pin_rec.ptr, self.records * RECORD_BYTES, 1, s)
+        d_out, off, ln = c.encode_batch_device(self.d_rec, self.rec_off, stream=s)
+        cd.memcpy_async(pin_files.ptr, d_out, int(off[-1] + ln[-1]), 2, s)
+        d_keys, n_keys = c.batch_sorted_keys()
+        d_recs, n_out, _ = c.decode_batch_device(d_out, off, ln, d_keys, n_keys, stream=s)
+        cd.memcpy_async(pin_recs.ptr, d_recs, n_out * RECORD_BYTES, 2, s)
+        cd.stream_sync(s)
+
+
+def run_lanes(lanes, fn, steps):
+    import threading
+
+    errs = []
+
+    def body(ln):
+        try:
+            for _ in range(steps):
+                fn(ln)
+            ln.cdcx.stream_sync(ln.stream)
+        except Exception as e:  # noqa: BLE001 - re-raised on the main thread
+            errs.append(e)
+
+    ts = [threading.Thread(target=body, args=(ln,)) for ln in lanes]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if errs:
+        raise errs[0]
+
+
 def main():
     args = parse()
     ws, rank, local = dist_env()
@@ -146,51 +211,71 @@ def main():
     B = args.ranks_per_gpu
     first = (rank * B) % args.world
     p = rempi_amd.default_gen_params(world_size=args.world, jitter=args.jitter, events_per_rank=args.events)
-    ctx = rempi_amd.Context(max_event_length=args.max_len, device=local)
-    d_rec, rec_off = ctx.generate_device(p, first, B)
-    n_records = int(rec_off[-1])
+    S = max(1, min(args.streams, B))
+    sizes = [B // S + (1 if i < B % S else 0) for i in range(S)]
+    lanes, f = [], first
+    for n in sizes:
+        lanes.append(Lane(args, p, f, n, local))
+        f += n
+    n_records = sum(ln.records for ln in lanes)
 
-    # The stream the library launches on: the default stream (NULL); its HIP events time
-    # each kernel (cdcx_set_profiling).
-    def step():
-        d_out, off, ln = ctx.encode_batch_device(d_rec, rec_off)
-        d_keys, n_keys = ctx.batch_sorted_keys()
-        _, n_out, _ = ctx.decode_batch_device(d_out, off, ln, d_keys, n_keys)
-        return int(ln.sum()), n_out
-
-    for _ in range(args.warmup):
-        step()
-    ctx.set_profiling(True)
-    ctx.reset_kernel_times()
+    run_lanes(lanes, Lane.step, args.warmup)
+    for ln in lanes:
+        ln.comp = 0
+        ln.ctx.set_profiling(True)
+        ln.ctx.reset_kernel_times()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    comp_bytes = 0
-    for _ in range(args.steps):
-        cb, n_out = step()
-        comp_bytes += cb
+    run_lanes(lanes, Lane.step, args.steps)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ctx.set_profiling(False)
-    ktimes = ctx.kernel_times()
+    ktimes = {}
+    for ln in lanes:
+        ln.ctx.set_profiling(False)
+        for k, (ms, nl) in ln.ctx.kernel_times().items():
+            a0, b0 = ktimes.get(k, (0.0, 0))
+            ktimes[k] = (a0 + ms, b0 + nl)
+    comp_bytes = sum(ln.comp for ln in lanes)
 
     # Verification outside the timed region: byte-exact vs the CPU oracle for a sample of
-    # ranks; decode(encode(x)) record round trip for the whole batch.
-    d_out, off, ln = ctx.encode_batch_device(d_rec, rec_off)
+    # ranks; decoded record count bounded by the input.
     fails = 0
-    for r in range(min(args.verify_ranks, B)):
-        host = rempi_amd.generate_host(p, first + r)
-        want, _ = O.encode(host, args.max_len)
-        got = cdcx.d2h(d_out + int(off[r]), int(ln[r])).tobytes()
-        fails += int(got != want)
-    d_keys, n_keys = ctx.batch_sorted_keys()
-    d_recs, n_out, _ = ctx.decode_batch_device(d_out, off, ln, d_keys, n_keys)
-    # round trip: decoded per-table streams are a permutation of the input records grouped by
-    # (chunk, table); compare multisets of (set, src, clock, with_next, index) of matched events
-    fails += int(n_out > n_records)
+    checked = 0
+    for ln in lanes:
+        d_out, off, ln_ = ln.step()
+        for r in range(ln.n):
+            if checked >= args.verify_ranks:
+                break
+            host = rempi_amd.generate_host(p, ln.first + r)
+            want, _ = O.encode(host, args.max_len)
+            got = cdcx.d2h(d_out + int(off[r]), int(ln_[r])).tobytes()
+            fails += int(got != want)
+            checked += 1
+        fails += int(ln.n_out > ln.records)
+
+    # Copy-inclusive rate (host memory in and out); never `value`.
+    host_io = None
+    if args.host_io and rank == 0:
+        pins = []
+        for ln in lanes:
+            pr = cdcx.PinnedBuffer(ln.records * RECORD_BYTES)
+            cdcx.memcpy_async(pr.ptr, ln.d_rec, ln.records * RECORD_BYTES, 2, ln.stream)
+            cdcx.stream_sync(ln.stream)
+            pins.append((pr, cdcx.PinnedBuffer(ln.records * 24 + (1 << 20)), cdcx.PinnedBuffer(ln.records * RECORD_BYTES)))
+        run_lanes(lanes, lambda ln: ln.host_io_step(*pins[lanes.index(ln)]), 1)
+        t1 = time.perf_counter()
+        run_lanes(lanes, lambda ln: ln.host_io_step(*pins[lanes.index(ln)]), args.host_io)
+        hio = time.perf_counter() - t1
+        host_io = {"value": round(n_records * RECORD_BYTES * args.host_io / hio / 1e9, 3), "unit": "GB/s",
+                   "steps": args.host_io,
+                   "what": "H2D records from pinned host memory + encode + decode + D2H rank files and decoded records"}
+        for pr in pins:
+            for b in pr:
+                b.close()
 
     counters = np.array([n_records * args.steps, comp_bytes, fails], dtype=np.float64)
     tmax = elapsed
@@ -207,17 +292,19 @@ def main():
     comp_per_event = counters[1] / total_records
 
     # Roofline of the dominant kernel: algorithmic bytes per launch / mean launch time.
-    enc_kernels = {k: v for k, v in ktimes.items() if v[1] > 0}
-    dom = max(enc_kernels, key=lambda k: enc_kernels[k][0])
-    dom_ms, dom_launches = enc_kernels[dom]
-    algo = algorithmic_bytes(dom, n_records, comp_per_event)
+    kern = {k: v for k, v in ktimes.items() if v[1] > 0}
+    dom = max(kern, key=lambda k: kern[k][0])
+    dom_ms, dom_launches = kern[dom]
+    per_launch_records = n_records / S
+    algo = algorithmic_bytes(dom, per_launch_records, comp_per_event)
     achieved = algo / (dom_ms / dom_launches / 1e3) / 1e9 if dom_launches else 0.0
 
     if args.kernel_report and rank == 0:
-        tot = sum(v[0] for v in enc_kernels.values())
-        for k, (ms, n) in sorted(enc_kernels.items(), key=lambda kv: -kv[1][0]):
+        tot = sum(v[0] for v in kern.values())
+        for k, (ms, n) in sorted(kern.items(), key=lambda kv: -kv[1][0]):
             print(f"  {k:22s} {ms / max(n, 1):10.3f} ms/launch x{n:4d}  {100 * ms / tot:5.1f}%", file=sys.stderr)
-        print(f"  timed {elapsed:.3f}s for {args.steps} steps; kernels sum {tot / 1e3:.3f}s", file=sys.stderr)
+        print(f"  timed {elapsed:.3f}s for {args.steps} steps on {S} streams; kernels sum {tot / 1e3:.3f}s",
+              file=sys.stderr)
 
     cpu = None
     if args.cpu_baseline and rank == 0 and ws == 1:
@@ -240,37 +327,51 @@ def main():
             "config": {"workload": f"config3: {args.world}-rank job, {args.events} events/rank traces, "
                                    f"{B} rank traces resident per GPU per step, encode+decode round trip",
                        "ranks_per_gpu": B, "events_per_rank": args.events, "records_per_step_per_gpu": n_records,
-                       "jitter": args.jitter, "rempi_max": args.max_len,
+                       "jitter": args.jitter, "rempi_max": args.max_len, "streams_per_gpu": S,
                        "compressed_bytes_per_event": round(comp_per_event, 3),
                        "parallelism": f"dp{ws} (independent rank traces per GPU)",
                        "verify_failures": int(counters[2])},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "launch_ms": round(dom_ms / dom_launches, 3),
+                         "algorithmic_bytes_per_launch": round(algo),
                          "pipeline_achieved": round(pipeline_bytes(comp_per_event) * total_records / tmax / 1e9, 2)},
             "cpu_baseline": cpu,
+            "host_io": host_io,
         }
         print(json.dumps(out))
+    for ln in lanes:
+        ln.ctx.close()
+        cdcx.stream_destroy(ln.stream)
     if dist:
         dist.destroy_process_group()
 
 
-# Algorithmic HBM bytes per record for each kernel (DESIGN.md "Kernels and their
-# rooflines"); c = compressed bytes per record.
+# Algorithmic HBM bytes per input record for each kernel (DESIGN.md §3 kernel tables); m =
+# matched fraction, c = compressed bytes per record.  The dominant kernel's figure is the
+# roofline numerator.
+M_FRAC = 0.833  # gen.h: one unmatched poll before 20 % of the calls -> 1 / 1.2 matched
+
+
 def algorithmic_bytes(kernel, n_records, c):
-    m = 0.86  # matched fraction of the synthetic workload (gen.h: 1 poll per 5 calls)
+    m = M_FRAC
     per = {
-        "k_scatter": 32 + 1 + 16 + 4,
-        "k_unit_prep": 16 + m * (8 + 4) + 0.3 * 12,
+        "k_tile_hist": 32,
+        "k_scatter": 32 + 16 + 4,
+        "k_unit_prep": 16 + m * (8 + 4),
         "k_sort_tiles": m * (8 + 8 + 4),
-        "k_rank_tiles": m * (8 + 4 + 4 + 4 + 8),
+        "k_rank_tiles": m * (8 + 4 + 8 + 4 + 4 + 8),
         "k_epoch": m * 8,
-        "k_chain_lane": m * (4 + 4 + 4 + 4 + 1),
-        "k_positions": m * (4 + 4 + 1 + 4 + 4 + 8 + 8),
-        "k_deltas": m * (4 + 1 + 4 + 4 + 8 + 4 + 4),
-        "k_write_units": m * (4 + 4 + 8 + 8) + c,
-        "k_dec_sections": c + m * 32,
-        "k_dec_perm_lane": m * (8 + 8 + 4 + 4 + 4),
-        "k_dec_records": c + m * (4 + 8 + 4) + 32,
+        "k_chain_grp16": m * (4 + 4 + 4),
+        "k_chain_grp64": m * (4 + 4 + 4),
+        "k_chain_mark": m * (4 + 1),
+        "k_positions": m * (4 + 1 + 4 + 4 + 4) / 2,
+        "k_deltas": m * (1.3 * 4 + 0.64 * (4 + 4 + 4)),
+        "k_write_units": m * (4 + 4 + 8) + c,
+        "k_write_keys": m * (8 + 8),
+        "k_dec_sections": 0.3 * c,
+        "k_dec_perm_grp": m * (0.64 * (8 + 16) + 8),
+        "k_dec_records": c + m * (4 + 8 + 8 + 1) + 32,
     }.get(kernel, 32)
     return per * n_records
 
@@ -278,7 +379,7 @@ def algorithmic_bytes(kernel, n_records, c):
 def pipeline_bytes(c):
     """encode reads 32 B/event and writes c; decode reads c + 8m of sorted keys
     and writes 32 B/event."""
-    return 64 + 2 * c + 8 * 0.86
+    return 64 + 2 * c + 8 * M_FRAC
 
 
 if __name__ == "__main__":

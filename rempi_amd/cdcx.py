@@ -282,7 +282,69 @@ def hip():
         _hip.hipMalloc.restype = ctypes.c_int
         _hip.hipFree.argtypes = [_vp]
         _hip.hipFree.restype = ctypes.c_int
+        _hip.hipStreamCreateWithFlags.argtypes = [P(_vp), ctypes.c_uint]
+        _hip.hipStreamCreateWithFlags.restype = ctypes.c_int
+        _hip.hipStreamSynchronize.argtypes = [_vp]
+        _hip.hipStreamSynchronize.restype = ctypes.c_int
+        _hip.hipStreamDestroy.argtypes = [_vp]
+        _hip.hipStreamDestroy.restype = ctypes.c_int
+        _hip.hipMemcpyAsync.argtypes = [_vp, _vp, ctypes.c_size_t, ctypes.c_int, _vp]
+        _hip.hipMemcpyAsync.restype = ctypes.c_int
+        _hip.hipHostMalloc.argtypes = [P(_vp), ctypes.c_size_t, ctypes.c_uint]
+        _hip.hipHostMalloc.restype = ctypes.c_int
+        _hip.hipHostFree.argtypes = [_vp]
+        _hip.hipHostFree.restype = ctypes.c_int
     return _hip
+
+
+def stream_create() -> int:
+    """A non-blocking HIP stream (hipStreamNonBlocking) as an integer handle."""
+    s = _vp()
+    rc = hip().hipStreamCreateWithFlags(ctypes.byref(s), 1)
+    if rc:
+        raise CdcxError(5, f"hipStreamCreateWithFlags failed ({rc})")
+    return s.value
+
+
+def stream_sync(stream: int) -> None:
+    rc = hip().hipStreamSynchronize(stream)
+    if rc:
+        raise CdcxError(5, f"hipStreamSynchronize failed ({rc})")
+
+
+def stream_destroy(stream: int) -> None:
+    hip().hipStreamDestroy(stream)
+
+
+def memcpy_async(dst: int, src: int, nbytes: int, kind: int, stream: int) -> None:
+    """kind: 1 host->device, 2 device->host, 3 device->device."""
+    if nbytes:
+        rc = hip().hipMemcpyAsync(dst, src, nbytes, kind, stream)
+        if rc:
+            raise CdcxError(5, f"hipMemcpyAsync failed ({rc})")
+
+
+class PinnedBuffer:
+    """Page-locked host memory (hipHostMalloc), for copy-inclusive measurements."""
+
+    def __init__(self, nbytes: int):
+        p = _vp()
+        rc = hip().hipHostMalloc(ctypes.byref(p), max(nbytes, 64), 0)
+        if rc:
+            raise CdcxError(7, f"hipHostMalloc of {nbytes} bytes failed ({rc})")
+        self.ptr = p.value
+        self.nbytes = nbytes
+
+    def close(self):
+        if self.ptr:
+            hip().hipHostFree(self.ptr)
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def d2h(ptr: int, nbytes: int, dtype=np.uint8) -> np.ndarray:

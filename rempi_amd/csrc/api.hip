@@ -399,8 +399,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int32_t* d_topg = c->buf<int32_t>("topg", N);
   int32_t* d_qn = c->buf<int32_t>("qn", N);
   int2* d_leaves = c->buf<int2>("leaves", w1n);
-  uint8_t* d_chain = c->buf<uint8_t>("chain", N);
-  HIPCHK(hipMemsetAsync(d_chain, 0, N, s));
+  uint8_t* d_chain = c->buf<uint8_t>("chain", N);  // every row written by k_chain_mark
   // Tiers: 16-lane groups; segments whose leaf list outgrows 16 slots go to 64-lane groups,
   // then to the lane kernel's exact global-memory path.  Each tier rewrites every output of
   // the segments it takes.
@@ -442,7 +441,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
             d_qexit, d_err);
   c->launch(K_CHAIN_ENTRIES, k_chain_entries, dim3(blocks(NU, 64)), dim3(64), s, d_units, NU, d_segs,
             (const int32_t*)d_qexit);
-  c->launch(K_CHAIN_MARK, k_chain_mark, dim3(blocks(nsegs, 256)), dim3(256), s, (const Unit*)d_units,
+  c->launch(K_CHAIN_MARK, k_chain_mark, dim3((unsigned)std::min<int64_t>(8192, blocks(nsegs, 4))), dim3(256), s, (const Unit*)d_units,
             (const Seg*)d_segs, (int32_t)nsegs, (const int32_t*)d_par, (const int32_t*)d_qn, d_chain);
   int32_t* d_posA = c->buf<int32_t>("posA", N);
   int32_t* d_crow = c->buf<int32_t>("crow", N);

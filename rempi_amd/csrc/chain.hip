@@ -450,20 +450,32 @@ __global__ void __launch_bounds__(64) k_chain_entries(Unit* __restrict__ units, 
   u.P = u.M - K;
 }
 
-// Mark the chain inside every segment: from its entry node down to relative level 1.
+// Mark the chain inside every segment (every row of the segment gets its flag, so the
+// flags need no clearing): from its entry node down to relative level 1.  One wave per
+// segment walks 64-row chunks of par from the top down (a parent's row is always below its
+// child's): the chunk is one coalesced load held one row per lane, each hop inside it is a
+// v_readlane instead of a dependent global load, and the chunk's flags are collected in a
+// lane mask and stored at once.
 __global__ void __launch_bounds__(256) k_chain_mark(const Unit* __restrict__ units, const Seg* __restrict__ segs,
                                                     int32_t nsegs, const int32_t* __restrict__ par,
                                                     const int32_t* __restrict__ qn, uint8_t* __restrict__ chain) {
-  const int si = blockIdx.x * 256 + threadIdx.x;
-  if (si >= nsegs) return;
-  const Seg sg = segs[si];
-  const int64_t a = units[sg.unit].a;
-  int32_t v = qn[a + sg.start + sg.entry];
-  while (true) {
-    chain[a + v] = 1;
-    const int32_t p = par[a + v];
-    if (p < 0) break;
-    v = p;
+  const int32_t nw = gridDim.x * 4;
+  const int l = lane_id();
+  for (int32_t si = blockIdx.x * 4 + wave_id(); si < nsegs; si += nw) {
+    const Seg sg = segs[si];
+    const int64_t a = units[sg.unit].a;
+    const int32_t s0 = sg.start, s1 = sg.start + sg.len;
+    int32_t want = qn[a + s0 + sg.entry];
+    for (int32_t c0 = s0 + ((s1 - 1 - s0) & ~63); c0 >= s0; c0 -= 64) {
+      const int32_t r = c0 + l;
+      const int32_t pv = (r < s1) ? par[a + r] : 0;
+      uint64_t mask = 0;
+      while (want >= c0) {
+        mask |= 1ull << (want - c0);
+        want = __builtin_amdgcn_readlane(pv, want - c0);
+      }
+      if (r < s1) chain[a + r] = (uint8_t)((mask >> l) & 1);
+    }
   }
 }
 
