@@ -415,7 +415,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     if (c->chain_tier <= 0) {
       c->launch(K_CHAIN_G16, k_chain_grp<16>, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, blocks(n, 64)))),
                 dim3(256), s, (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par,
-                d_exta, d_topg, d_qn, d_ovf1, d_cnt + 1, d_err);
+                d_exta, d_topg, d_qn, d_ovf1, d_cnt + 1, d_err, getenv("CDCX_CXMODE") ? atoi(getenv("CDCX_CXMODE")) : 0);
       list = d_ovf1;
       nlist = d_cnt + 1;
       n = c->download(d_cnt + 1, 1, s)[0];
@@ -424,7 +424,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     c->chain_tier_counts[1] = n;
     if (n > 0 && c->chain_tier <= 1) {
       c->launch(K_CHAIN_G64, k_chain_grp<64>, dim3((unsigned)blocks(n, 4)), dim3(256), s, (const Unit*)d_units, d_segs, list,
-                nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par, d_exta, d_topg, d_qn, d_ovf2, d_cnt + 2, d_err);
+                nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par, d_exta, d_topg, d_qn, d_ovf2, d_cnt + 2, d_err, 0);
       list = d_ovf2;
       n = c->download(d_cnt + 2, 1, s)[0];
     }

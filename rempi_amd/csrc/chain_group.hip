@@ -84,7 +84,8 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
                                                    const int32_t* __restrict__ cord, const int32_t* __restrict__ inv,
                                                    int32_t* __restrict__ par, int32_t* __restrict__ exta,
                                                    int32_t* __restrict__ topg, int32_t* __restrict__ qn,
-                                                   int32_t* __restrict__ ovf, int32_t* __restrict__ novf, uint32_t* err) {
+                                                   int32_t* __restrict__ ovf, int32_t* __restrict__ novf, uint32_t* err,
+                                                   int32_t xmode) {
   using Gr = Grp<G>;
   using Mask = typename Gr::Mask;
   constexpr int kGroups = 256 / G;
@@ -105,7 +106,7 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
   int32_t lid = 0, llv = 0, lcol = 0, top = 0, cw0 = 0, cw1 = 0, iw0 = 0, iw1 = 0, pval = 0;
 
   auto node = [&](int32_t x) -> int2 {  // {par, column} of row x < i of this segment
-    if (x >= i - R) return ring[x & (R - 1)];
+    if (x >= i - R || (xmode & 1)) return ring[x & (R - 1)];
     return make_int2(par[a + x], cord[a + x]);
   };
 
@@ -144,7 +145,9 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
       cw1 = (cb + G + j < s1) ? cord[a + cb + G + j] : 0;
     }
     const int32_t t = i - cb;
-    const int32_t c = Gr::at(cw0, t);
+    // c of row i: lane 0 of the window, which shifts down one lane per row (DPP, no LDS trip)
+    const int32_t c = Gr::first(cw0);
+    cw0 = Gr::from_next(cw0);
 
     // ---- k*: highest level whose top column is smaller than c ---------------------------
     const Mask tm = Gr::ballot(j < lmax && top < c);
@@ -282,8 +285,8 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
 }
 
 template __global__ void k_chain_grp<16>(const Unit*, Seg*, const int32_t*, const int32_t*, const int32_t*, const int32_t*,
-                                         int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*);
+                                         int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*, int32_t);
 template __global__ void k_chain_grp<64>(const Unit*, Seg*, const int32_t*, const int32_t*, const int32_t*, const int32_t*,
-                                         int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*);
+                                         int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*, int32_t);
 
 }  // namespace cdcx
