@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--world", type=int, default=1024, help="ranks in the traced job")
     ap.add_argument("--events", type=int, default=10_000_000, help="events per rank trace")
-    ap.add_argument("--ranks-per-gpu", type=int, default=32, help="rank traces resident per GPU (one step)")
+    ap.add_argument("--ranks-per-gpu", type=int, default=64, help="rank traces resident per GPU (one step)")
     ap.add_argument("--jitter", type=int, default=8)
     ap.add_argument("--max-len", type=int, default=131072, help="REMPI_MAX")
     ap.add_argument("--verify-ranks", type=int, default=1, help="ranks checked byte-exact vs the CPU oracle")
@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--cpu-sample-events", type=int, default=1_000_000)
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--kernel-report", action="store_true", help="print per-kernel times to stderr")
-    ap.add_argument("--streams", type=int, default=2, help="rank batches in flight per GPU (one HIP stream each)")
+    ap.add_argument("--streams", type=int, default=4, help="rank batches in flight per GPU (one HIP stream each)")
     ap.add_argument("--host-io", type=int, default=1, help="steps of the copy-inclusive measurement (0 = skip)")
     return ap.parse_args()
 
@@ -233,6 +233,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    free_b, total_b = torch.cuda.mem_get_info()
     ktimes = {}
     for ln in lanes:
         ln.ctx.set_profiling(False)
@@ -329,6 +330,7 @@ def main():
                        "ranks_per_gpu": B, "events_per_rank": args.events, "records_per_step_per_gpu": n_records,
                        "jitter": args.jitter, "rempi_max": args.max_len, "streams_per_gpu": S,
                        "compressed_bytes_per_event": round(comp_per_event, 3),
+                       "hbm_used_gb": round((total_b - free_b) / 1e9, 1),
                        "parallelism": f"dp{ws} (independent rank traces per GPU)",
                        "verify_failures": int(counters[2])},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

@@ -121,7 +121,9 @@ int cdcx_reconstruct_stream(cdcx_ctx* ctx, const uint8_t* in, size_t len,
  * context-owned device buffers:
  *   *d_rec_out  reconstructed records (int32 x 8), units in file order
  *   *n_rec_out  number of records
- *   *d_perm     per-unit matched_events_permutated_indices, concatenated (int32) */
+ *   *d_perm     per-unit matched_events_permutated_indices, concatenated (int32)
+ * They stay valid until the next encode or decode call on ctx (decode scratch reuses the
+ * encoder's scratch; the encoder's *d_out and sorted keys are not touched by decode). */
 int cdcx_decode_batch_device(cdcx_ctx* ctx, int32_t n_ranks, const uint8_t* d_in,
                              const int64_t* in_off, const int64_t* in_len,
                              const int32_t* d_keys, int64_t n_keys,

@@ -59,6 +59,17 @@ struct DevBuf {
 
 inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
+// Decode scratch lives in encode scratch that is dead by then (one context = one stream,
+// encode and decode never overlap): grow-only named buffers shared by both phases.
+constexpr const char* kAliasRecs = "trec";    // decoded records       <- T-order records
+constexpr const char* kAliasIdd = "mkey";     // pair ids              <- observed-order keys
+constexpr const char* kAliasDld = "skey";     // pair delays           <- clock-order keys
+constexpr const char* kAliasWpd = "run_cnt";  // with_previous         <- unmatched run counts
+constexpr const char* kAliasUidd = "ep_rank"; // unmatched ids         <- epoch ranks
+constexpr const char* kAliasPerm = "cord";    // perm                  <- clock order of rows
+constexpr const char* kAliasCinv = "inv";     // perm^-1               <- row of each clock
+constexpr const char* kAliasWnf = "chain";    // with_next flags       <- chain flags
+
 }  // namespace
 
 struct cdcx_ctx {
@@ -398,7 +409,6 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int32_t* d_exta = c->buf<int32_t>("exta", N);
   int32_t* d_topg = c->buf<int32_t>("topg", N);
   int32_t* d_qn = c->buf<int32_t>("qn", N);
-  int2* d_leaves = c->buf<int2>("leaves", w1n);
   uint8_t* d_chain = c->buf<uint8_t>("chain", N);  // every row written by k_chain_mark
   // Tiers: 16-lane groups; segments whose leaf list outgrows 16 slots go to 64-lane groups,
   // then to the lane kernel's exact global-memory path.  Each tier rewrites every output of
@@ -428,6 +438,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
       list = d_ovf2;
       n = c->download(d_cnt + 2, 1, s)[0];
     }
+    int2* d_leaves = n > 0 ? c->buf<int2>("leaves", w1n) : nullptr;  // lane tier only
     if (n > 0)
       c->launch(K_CHAIN_SEG, k_chain_seg<16>, dim3((unsigned)std::min<int64_t>(1024, blocks(n, 256))), dim3(256), s,
                 (const Unit*)d_units, d_segs, (int32_t)n, list, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par,
@@ -587,21 +598,19 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   if (records && n_keys < ko) throw CdcxError{CDCX_ERR_ARG, "fewer sorted keys than matched events in the files"};
   d_units = c->upload("d_units", units, s);
   c->dunits = units;
-  uint64_t* d_wpd = c->buf<uint64_t>("d_wpd", wb);
-  uint64_t* d_uidd = c->buf<uint64_t>("d_uidd", wb);
-  uint64_t* d_idd = c->buf<uint64_t>("d_idd", wb);  // written by k_dec_perm_grp
-  uint64_t* d_dld = c->buf<uint64_t>("d_dld", wb);
-  int32_t* d_nx = c->buf<int32_t>("d_nx", wb);
-  int32_t* d_pv = c->buf<int32_t>("d_pv", wb);
-  int32_t* d_perm = c->buf<int32_t>("d_perm", ko);
-  uint8_t* d_wnf = c->buf<uint8_t>("d_wnf", wb);
+  uint64_t* d_wpd = c->buf<uint64_t>(kAliasWpd, wb);
+  uint64_t* d_uidd = c->buf<uint64_t>(kAliasUidd, wb);
+  uint64_t* d_idd = c->buf<uint64_t>(kAliasIdd, wb);  // written by k_dec_perm_grp
+  uint64_t* d_dld = c->buf<uint64_t>(kAliasDld, wb);
+  int32_t* d_perm = c->buf<int32_t>(kAliasPerm, ko);
+  uint8_t* d_wnf = c->buf<uint8_t>(kAliasWnf, wb);
   HIPCHK(hipMemsetAsync(d_wnf, 0, wb, s));
   c->launch(K_DEC_SECTIONS, k_dec_sections, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, d_wpd, d_uidd, d_wnf,
             d_err);
   // Permutation rebuild (decode.hip): 16-lane groups with LDS ring windows, which also invert
   // the pair sections' LP; then the 256-slot settle-when-full window, then the sequential
   // list for whatever is left.
-  int32_t* d_cinv = c->buf<int32_t>("d_cinv", ko);
+  int32_t* d_cinv = c->buf<int32_t>(kAliasCinv, ko);
   int32_t* d_nfail = c->buf<int32_t>("d_nfail", 2);
   HIPCHK(hipMemsetAsync(d_nfail, 0, 8, s));
   {
@@ -617,9 +626,12 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
     c->launch(K_DEC_WIN4, k_dec_perm_window<4>, dim3(NU), dim3(64), s, d_units, NU, 1, (const uint64_t*)d_idd,
               (const uint64_t*)d_dld, d_perm, d_nfail + 1);
     const int32_t nf2 = c->dec_tier > 1 ? NU : c->download(d_nfail + 1, 1, s)[0];
-    if (nf2 > 0)
+    if (nf2 > 0) {
+      int32_t* d_nx = c->buf<int32_t>("d_nx", wb);  // the sequential list only exists when needed
+      int32_t* d_pv = c->buf<int32_t>("d_pv", wb);
       c->launch(K_DEC_PERM, k_dec_perm_lane, dim3(blocks(NU, 64)), dim3(64), s, (const DUnit*)d_units, NU,
                 (const uint64_t*)d_idd, (const uint64_t*)d_dld, d_nx, d_pv, d_perm, d_err);
+    }
     c->launch(K_DEC_PERM, k_dec_cinv, dim3(NU), dim3(256), s, (const DUnit*)d_units, (const int32_t*)d_perm, d_cinv);
     nf = nf2;
   }
@@ -638,7 +650,7 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
       for (int32_t k = 0; k < nt; k++) rt.push_back(make_int2(q, k));
     }
     int2* d_rt = c->upload("d_rec_tiles", rt, s);
-    int32_t* d_recs = c->buf<int32_t>("d_recs", 8 * ro);
+    int32_t* d_recs = c->buf<int32_t>(kAliasRecs, 8 * ro);
     c->launch(K_DEC_RECORDS, k_dec_records, dim3((unsigned)rt.size()), dim3(256), s, (const DUnit*)d_units,
               (const int2*)d_rt, d_in, (const int32_t*)d_cinv, (const uint8_t*)d_wnf, (const uint64_t*)d_uidd, d_keys,
               (int4*)d_recs);
@@ -653,10 +665,10 @@ std::vector<int64_t> tables_dump(cdcx_ctx* c, const uint8_t* in, hipStream_t s) 
   const size_t NU = c->dunits.size();
   int64_t wb = 0, ko = 0;
   for (auto& u : c->dunits) { wb = std::max(wb, u.wbase + u.M + 1); ko = std::max(ko, u.key_off + u.M); }
-  std::vector<uint64_t> wpd = c->download(c->buf<uint64_t>("d_wpd", 0), wb, s);
-  std::vector<uint64_t> uidd = c->download(c->buf<uint64_t>("d_uidd", 0), wb, s);
-  std::vector<uint64_t> idd = c->download(c->buf<uint64_t>("d_idd", 0), wb, s);
-  std::vector<uint64_t> dld = c->download(c->buf<uint64_t>("d_dld", 0), wb, s);
+  std::vector<uint64_t> wpd = c->download(c->buf<uint64_t>(kAliasWpd, 0), wb, s);
+  std::vector<uint64_t> uidd = c->download(c->buf<uint64_t>(kAliasUidd, 0), wb, s);
+  std::vector<uint64_t> idd = c->download(c->buf<uint64_t>(kAliasIdd, 0), wb, s);
+  std::vector<uint64_t> dld = c->download(c->buf<uint64_t>(kAliasDld, 0), wb, s);
   std::vector<int32_t> perm = c->download(c->d_perm, ko, s);
   (void)NU;
   std::vector<int64_t> d;
