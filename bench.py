@@ -208,11 +208,12 @@ def main():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
 
-    B = args.ranks_per_gpu
-    first = (rank * B) % args.world
+    from rempi_amd import shard
+
+    first, B = shard.shard(args.world, ws, rank, args.ranks_per_gpu)
     p = rempi_amd.default_gen_params(world_size=args.world, jitter=args.jitter, events_per_rank=args.events)
-    S = max(1, min(args.streams, B))
-    sizes = [B // S + (1 if i < B % S else 0) for i in range(S)]
+    sizes = shard.lane_sizes(B, args.streams)
+    S = len(sizes)
     lanes, f = [], first
     for n in sizes:
         lanes.append(Lane(args, p, f, n, local))
@@ -278,15 +279,7 @@ def main():
             for b in pr:
                 b.close()
 
-    counters = np.array([n_records * args.steps, comp_bytes, fails], dtype=np.float64)
-    tmax = elapsed
-    if dist:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        tmax = float(t.item())
-        c = torch.tensor(counters, device="cuda")
-        dist.all_reduce(c)
-        counters = c.cpu().numpy()
+    counters, tmax = shard.reduce_counters([n_records * args.steps, comp_bytes, fails], elapsed, dist, "cuda")
 
     total_records = counters[0]
     value = total_records * RECORD_BYTES / tmax / 1e9
