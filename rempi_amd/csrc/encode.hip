@@ -379,43 +379,89 @@ __global__ void __launch_bounds__(256) k_unit_prep(Unit* __restrict__ units, con
 __global__ void __launch_bounds__(256) k_sort_tiles(const Unit* __restrict__ units, const SortTile* __restrict__ st,
                                                     const uint64_t* __restrict__ mkey, uint64_t* __restrict__ tkey,
                                                     int32_t* __restrict__ lrank, uint64_t* __restrict__ tminmax) {
-  __shared__ uint64_t key[kSortTile];
-  __shared__ int16_t idx[kSortTile];
+  // Bitonic network held in registers: thread t owns elements 4t..4t+3.  Strides 1 and 2
+  // compare inside a thread, strides 4..128 exchange with lane t ^ (stride/4) of the same
+  // wave (shuffles), and only strides 256 and 512 (3 of the 55 stages) go through LDS.
+  // Order: (key, original index), so equal keys keep row order.
+  __shared__ uint64_t xk[kSortTile];
+  __shared__ int32_t xi[kSortTile];
   const SortTile w = st[blockIdx.x];
   const Unit u = units[w.unit];
   const int64_t base = u.a + (int64_t)w.tile * kSortTile;
   const int len = min(kSortTile, u.M - w.tile * kSortTile);
-  for (int j = threadIdx.x; j < kSortTile; j += 256) {
-    key[j] = (j < len) ? mkey[base + j] : ~0ull;
-    idx[j] = (int16_t)j;
+  const int t = threadIdx.x;
+  uint64_t vk[4];
+  int32_t vi[4];
+  auto gt = [](uint64_t ak, int32_t ai, uint64_t bk, int32_t bi) { return ak > bk || (ak == bk && ai > bi); };
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int e = 4 * t + q;
+    vk[q] = (e < len) ? mkey[base + e] : ~0ull;
+    vi[q] = e;
   }
-  __syncthreads();
   for (int size = 2; size <= kSortTile; size <<= 1) {
+    const bool asc = ((4 * t) & size) == 0;  // the same for all four elements when size >= 4
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int p = threadIdx.x; p < kSortTile / 2; p += 256) {
-        const int i = 2 * p - (p & (stride - 1));
-        const int j = i + stride;
-        const bool up = ((i & size) == 0);
-        const uint64_t ki = key[i], kj = key[j];
-        const int16_t ii = idx[i], ij = idx[j];
-        const bool gt = (ki > kj) || (ki == kj && ii > ij);
-        if (gt == up) {
-          key[i] = kj;
-          key[j] = ki;
-          idx[i] = ij;
-          idx[j] = ii;
+      if (stride >= 4) {
+        uint64_t ok[4];
+        int32_t oi[4];
+        if (stride >= 256) {
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            xk[4 * t + q] = vk[q];
+            xi[4 * t + q] = vi[q];
+          }
+          __syncthreads();
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            ok[q] = xk[(4 * t + q) ^ stride];
+            oi[q] = xi[(4 * t + q) ^ stride];
+          }
+          __syncthreads();
+        } else {
+          const int sl = stride >> 2;
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            ok[q] = __shfl_xor(vk[q], sl, 64);
+            oi[q] = __shfl_xor(vi[q], sl, 64);
+          }
+        }
+        // keep the min when this element is the lower of an ascending pair or the upper of
+        // a descending one
+        const bool keep_min = (((4 * t) & stride) == 0) == asc;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          if (keep_min == gt(vk[q], vi[q], ok[q], oi[q])) {
+            vk[q] = ok[q];
+            vi[q] = oi[q];
+          }
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          if (q & stride) continue;  // q is the lower element of the pair (q, q + stride)
+          const bool a2 = (size == 2) ? (((4 * t + q) & 2) == 0) : asc;
+          if (gt(vk[q], vi[q], vk[q + stride], vi[q + stride]) == a2) {
+            const uint64_t tk = vk[q];
+            const int32_t ti = vi[q];
+            vk[q] = vk[q + stride];
+            vi[q] = vi[q + stride];
+            vk[q + stride] = tk;
+            vi[q + stride] = ti;
+          }
         }
       }
-      __syncthreads();
     }
   }
-  for (int r = threadIdx.x; r < len; r += 256) {
-    tkey[base + r] = key[r];
-    lrank[base + idx[r]] = r;
-  }
-  if (threadIdx.x == 0) {
-    tminmax[2 * (u.sort_tile0 + w.tile)] = key[0];
-    tminmax[2 * (u.sort_tile0 + w.tile) + 1] = key[len - 1];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int r = 4 * t + q;
+    if (r < len) {
+      tkey[base + r] = vk[q];
+      lrank[base + vi[q]] = r;
+    }
+    if (r == 0) tminmax[2 * (u.sort_tile0 + w.tile)] = vk[q];
+    if (r == len - 1) tminmax[2 * (u.sort_tile0 + w.tile) + 1] = vk[q];
   }
 }
 
