@@ -383,7 +383,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
             d_inv, d_skey);
   uint64_t* d_ep_rank = c->buf<uint64_t>("ep_rank", N);
   uint64_t* d_ep_clk = c->buf<uint64_t>("ep_clk", N);
-  c->launch(K_EPOCH, k_epoch, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, d_err);
+  c->launch(K_EPOCH, k_epoch<512>, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, d_err);
   // Chain: closed-prefix segments simulated independently, then stitched (chain.hip).
   int32_t* d_segend = c->buf<int32_t>("segend", N);
   c->launch(K_CUTS, k_cuts, dim3(NU), dim3(256), s, d_units, (const int32_t*)d_cord, d_segend);
@@ -396,6 +396,9 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   }
   if (nsegs > INT32_MAX) throw CdcxError{CDCX_ERR_LIMIT, "too many segments in one batch"};
   d_units = c->upload("units", units, s);
+  if (std::any_of(units.begin(), units.end(), [](const Unit& u) { return u.S == -1; }))  // > 256 sources
+    c->launch(K_EPOCH, k_epoch<2 * kMaxUnitSources>, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank,
+              d_ep_clk, d_err);
   Seg* d_segs = c->buf<Seg>("segs", nsegs);
   c->launch(K_SEG_LIST, k_seg_list, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_segend, d_segs);
   int32_t* d_seghist = c->buf<int32_t>("seghist", 4096);

@@ -575,16 +575,23 @@ __global__ void __launch_bounds__(256) k_rank_tiles(const Unit* __restrict__ uni
 // Epoch line (format(), :246-267): per source the last clock in sorted order, listed in
 // the iteration order of the reference's unordered_map<size_t,size_t> fed in sorted
 // order.  Also the clock-order check of :249-256 (equal (clock, source) keys, clock != 0).
+//
+// Two instances: HCAP = 512 (up to 256 distinct sources per table, 9 KB of LDS, so a CU
+// runs 8 blocks) for every unit, and HCAP = 2 * kMaxUnitSources (72 KB of LDS) only for the
+// units the small one marks with S = -1.
+template <int HCAP>
 __global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const uint64_t* __restrict__ skey,
                                                uint64_t* __restrict__ ep_rank, uint64_t* __restrict__ ep_clk,
                                                uint32_t* err) {
-  constexpr int HCAP = 2 * kMaxUnitSources;
+  constexpr int LCAP = HCAP / 2;  // distinct sources this instance can list
+  constexpr bool kBig = HCAP >= 2 * kMaxUnitSources;
   __shared__ int32_t hsrc[HCAP];
   __shared__ int32_t hpos[HCAP];
   __shared__ int32_t hclk[HCAP];
   __shared__ int32_t nlist;
   // After compaction the hash arrays are reused as the sort buffers and emulator storage.
   Unit& u = units[blockIdx.x];
+  if (kBig && u.S != -1) return;
   const int64_t a = u.a;
   const int32_t M = u.M;
   for (int i = threadIdx.x; i < HCAP; i += 256) {
@@ -597,7 +604,7 @@ __global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const u
   for (int32_t r = threadIdx.x; r < M; r += 256) {
     const uint64_t k = skey[a + r];
     const int32_t src = key_source(k), clk = key_clock(k);
-    if (r + 1 < M && skey[a + r + 1] == k && clk != 0) raise_error(err, kErrClockOrder);
+    if (!kBig && r + 1 < M && skey[a + r + 1] == k && clk != 0) raise_error(err, kErrClockOrder);
     if (src == INT32_MIN) { raise_error(err, kErrLimit); continue; }
     uint32_t h = ((uint32_t)src * 2654435761u) % HCAP;
     for (int probe = 0; probe < HCAP; probe++) {
@@ -612,13 +619,13 @@ __global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const u
   }
   __syncthreads();
   // Compact (src, first sorted position, last clock) triples.
-  __shared__ int32_t lpos[kMaxUnitSources];
-  __shared__ int32_t lsrc[kMaxUnitSources];
-  __shared__ int32_t lclk[kMaxUnitSources];
+  __shared__ int32_t lpos[LCAP];
+  __shared__ int32_t lsrc[LCAP];
+  __shared__ int32_t lclk[LCAP];
   for (int i = threadIdx.x; i < HCAP; i += 256) {
     if (hsrc[i] != INT32_MIN) {
       int q = atomicAdd(&nlist, 1);
-      if (q < kMaxUnitSources) {
+      if (q < LCAP) {
         lpos[q] = hpos[i];
         lsrc[q] = hsrc[i];
         lclk[q] = hclk[i];
@@ -627,8 +634,15 @@ __global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const u
   }
   __syncthreads();
   const int S = nlist;
-  if (S > kMaxUnitSources) {
-    if (threadIdx.x == 0) { raise_error(err, kErrLimit); u.S = 0; }
+  if (S > LCAP) {
+    if (threadIdx.x == 0) {
+      if (kBig) {
+        raise_error(err, kErrLimit);
+        u.S = 0;
+      } else {
+        u.S = -1;  // more sources than the small table holds: the big instance redoes it
+      }
+    }
     return;
   }
   int P2 = 1;
@@ -666,6 +680,9 @@ __global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const u
     u.S = S;
   }
 }
+
+template __global__ void k_epoch<512>(Unit*, const uint64_t*, uint64_t*, uint64_t*, uint32_t*);
+template __global__ void k_epoch<2 * kMaxUnitSources>(Unit*, const uint64_t*, uint64_t*, uint64_t*, uint32_t*);
 
 // ---------------------------------------------------------------------------------------
 // Edit-sequence positions (A8).  With chain rows r_1<..<r_K (columns col_k) and r_0 =

@@ -85,6 +85,17 @@ def test_random_streams_vs_oracle():
     assert not bad, bad[:5]
 
 
+@pytest.mark.parametrize("senders", [255, 257, 700])
+def test_many_sources_per_table(senders):
+    """Epoch lines with more distinct sources per table than the small LDS hash holds (256)
+    take the large-table kernel; the bytes and the footer order stay the reference's."""
+    recs = S.gen_stream(senders, 6 * senders, n_sets=1, n_senders=senders, jitter=8)
+    want, _ = O.encode(recs, 131072)
+    got = ctx(131072).encode_stream(recs)
+    assert got == want, first_diff(got, want)
+    assert ctx(131072).decode_stream(want) == O.decode(want)
+
+
 def test_encode_chunk_payload():
     rng = np.random.default_rng(5)
     for t in range(20):
