@@ -287,11 +287,11 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   c->launch(K_HIST_SCAN, k_hist_scan, dim3(R), dim3(256), s, (const uint32_t*)d_hist, (const int32_t*)d_tile0,
             (const int32_t*)d_ntiles, (const int32_t*)d_nsets, (const int32_t*)d_setlist, (const int64_t*)d_rec_off, d_base,
             d_tstart, d_tfirst);
+  int32_t* d_s2t = c->buf<int32_t>("lrank", N);  // stream -> T-order; dead before the tile sort needs "lrank"
   c->launch(K_SCATTER, k_scatter, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, (const int16_t*)d_dense,
-            (const int32_t*)d_base, (const int64_t*)d_rec_off, d_trec, d_t2s);
-  c->launch(K_INC0, k_inc0, dim3(NT), dim3(256), s, (const TRec*)d_trec, (const int32_t*)d_t2s, (const uint8_t*)d_tfirst,
-            (const Tile*)d_tiles, (const int64_t*)d_rec_off, d_inc0);
-  c->launch(K_TILE_SUM, k_tile_sum, dim3(NT), dim3(256), s, (const uint8_t*)d_inc0, (const Tile*)d_tiles, d_tsum);
+            (const int32_t*)d_base, (const int64_t*)d_rec_off, d_trec, d_t2s, d_s2t);
+  c->launch(K_INC0, k_inc0, dim3(NT), dim3(256), s, (const TRec*)d_trec, (const int32_t*)d_s2t, (const uint8_t*)d_tfirst,
+            (const Tile*)d_tiles, (const int64_t*)d_rec_off, d_inc0, d_tsum);
   c->launch(K_RANK_SCAN, k_rank_scan, dim3(R), dim3(256), s, (const int32_t*)d_tsum, (const int32_t*)d_tile0,
             (const int32_t*)d_ntiles, d_toff);
   c->launch(K_TILE_P0, k_tile_p0, dim3(NT), dim3(256), s, (const uint8_t*)d_inc0, (const Tile*)d_tiles,

@@ -89,7 +89,7 @@ __global__ void __launch_bounds__(256) k_hist_scan(const uint32_t* __restrict__ 
 __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
                                                  const int16_t* __restrict__ dense, const int32_t* __restrict__ base,
                                                  const int64_t* __restrict__ rec_off, TRec* __restrict__ trec,
-                                                 int32_t* __restrict__ t2s) {
+                                                 int32_t* __restrict__ t2s, int32_t* __restrict__ s2t) {
   constexpr int ROUNDS = kTile / 256;
   __shared__ int32_t wc[ROUNDS * 4 * kMaxSets];  // [round][wave][table]
   for (int i = threadIdx.x; i < ROUNDS * 4 * kMaxSets; i += 256) wc[i] = 0;
@@ -156,34 +156,32 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
     o.info = matched ? (0x80000000u | (hi[j].x != 0 ? 1u : 0u)) : 0u;
     trec[rb + pos] = o;
     t2s[rb + pos] = spos0 + i;
+    s2t[t.start + i] = pos;
   }
 }
 
 // inc0: length increment of each record if chunks were infinite (add(), :189-212): 1 for a
 // matched event, 1 for an unmatched event that starts a new run of its table, else 0.
-// Scattered back to stream order.
-__global__ void __launch_bounds__(256) k_inc0(const TRec* __restrict__ trec, const int32_t* __restrict__ t2s,
+// Walked in stream order (the T-order position comes from s2t), so the flags are written
+// coalesced and the T-order reads advance sequentially per table; the tile's sum is formed
+// here too.
+__global__ void __launch_bounds__(256) k_inc0(const TRec* __restrict__ trec, const int32_t* __restrict__ s2t,
                                               const uint8_t* __restrict__ tfirst, const Tile* __restrict__ tiles,
-                                              const int64_t* __restrict__ rec_off, uint8_t* __restrict__ inc0s) {
-  const Tile t = tiles[blockIdx.x];
-  const int64_t rb = rec_off[t.rank];
-  for (int i = threadIdx.x; i < t.len; i += blockDim.x) {
-    const int64_t k = t.start + i;
-    const bool m = trec[k].info >> 31;
-    uint8_t inc = 1;
-    if (!m && !tfirst[k] && !(trec[k - 1].info >> 31)) inc = 0;
-    inc0s[rb + t2s[k]] = inc;
-  }
-}
-
-__global__ void __launch_bounds__(256) k_tile_sum(const uint8_t* __restrict__ v, const Tile* __restrict__ tiles,
-                                                  int32_t* __restrict__ tsum) {
+                                              const int64_t* __restrict__ rec_off, uint8_t* __restrict__ inc0s,
+                                              int32_t* __restrict__ tsum) {
   __shared__ int32_t lds[4];
   const Tile t = tiles[blockIdx.x];
-  int32_t s = 0;
-  for (int i = threadIdx.x; i < t.len; i += blockDim.x) s += v[t.start + i];
-  s = block_sum<256>(s, lds);
-  if (threadIdx.x == 0) tsum[blockIdx.x] = s;
+  const int64_t rb = rec_off[t.rank];
+  int32_t sum = 0;
+  for (int i = threadIdx.x; i < t.len; i += blockDim.x) {
+    const int64_t g = rb + s2t[t.start + i];
+    uint8_t inc = 1;
+    if (!(trec[g].info >> 31) && !tfirst[g] && !(trec[g - 1].info >> 31)) inc = 0;
+    inc0s[t.start + i] = inc;
+    sum += inc;
+  }
+  sum = block_sum<256>(sum, lds);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = sum;
 }
 
 __global__ void __launch_bounds__(256) k_rank_scan(const int32_t* __restrict__ tsum, const int32_t* __restrict__ tile0,
