@@ -845,25 +845,38 @@ __global__ void __launch_bounds__(256) k_deltas(const Unit* __restrict__ units, 
   const uint32_t* sq = seq + 2 * a;
   const int32_t L = 2 * u.P + u.K;
   const int g = threadIdx.x >> 4, j = threadIdx.x & 15, gw = (threadIdx.x >> 4) & 3;
+  const int32_t* sxa = sx + 2 * a;
   int32_t ck = 0;
+  // this round's sequence entries and ids; the next round's are loaded while the spans of
+  // this one are counted
+  uint32_t e[4];
+  int32_t xs[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int32_t z = 4 * threadIdx.x + q;
+    e[q] = (z < L) ? sq[z] : kIgn;
+    xs[q] = (z < L) ? sxa[z] : 0;
+  }
   for (int32_t b = 0; b < L; b += 1024) {
     const int32_t q0 = b + 4 * threadIdx.x;
-    uint32_t e[4];
     int32_t v = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      e[q] = (q0 + q < L) ? sq[q0 + q] : kIgn;
+    for (int q = 0; q < 4; q++)
       if ((e[q] & 3) != kIgn && (int32_t)(e[q] >> 2) < q0 + q) v++;
-    }
     int32_t tot;
     int32_t k = block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       ring[(q0 + q) & (RING - 1)] = e[q];
-      if ((e[q] & 3) != kIgn && (int32_t)(e[q] >> 2) < q0 + q)
-        items[k++] = make_int4(q0 + q, (int32_t)e[q], sx[2 * a + q0 + q], 0);
+      if ((e[q] & 3) != kIgn && (int32_t)(e[q] >> 2) < q0 + q) items[k++] = make_int4(q0 + q, (int32_t)e[q], xs[q], 0);
     }
     __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int32_t z = q0 + 1024 + q;
+      e[q] = (z < L) ? sq[z] : kIgn;
+      xs[q] = (z < L) ? sxa[z] : 0;
+    }
     const int32_t rlo = b + 1024 - RING;  // entries >= rlo are in the ring
     // one item per 16-lane group: the group counts its span 16 entries at a time
     for (int32_t it = g; it < tot; it += 16) {
@@ -872,19 +885,23 @@ __global__ void __launch_bounds__(256) k_deltas(const Unit* __restrict__ units, 
       int32_t d = 0;
       for (int32_t z0 = f + 1; z0 < s; z0 += 16) {
         const int32_t z = z0 + j;
-        bool c = false;
-        if (z < s) {
-          const uint32_t y = (z >= rlo) ? ring[z & (RING - 1)] : sq[z];
-          const uint32_t yt = y & 3;
-          const int32_t pt = (int32_t)(y >> 2);
-          c = (yt == kIgn) | ((yt == kRem) & (pt > s)) | ((yt == kAdd) & (pt < s));
-        }
+        uint32_t y = ring[z & (RING - 1)];
+        // entries older than the ring (spans longer than ~3 K) come from memory, behind a
+        // wave-uniform branch so that the common case issues no global load at all
+        if (__builtin_amdgcn_ballot_w64(z < s && z < rlo))
+          if (z < s && z < rlo) y = sq[z];
+        const uint32_t yt = y & 3;
+        const int32_t pt = (int32_t)(y >> 2);
+        const bool c = (z < s) & ((yt == kIgn) | ((yt == kRem) & (pt > s)) | ((yt == kAdd) & (pt < s)));
         d += __popc((uint32_t)(__ballot(c) >> (16 * gw)) & 0xFFFFu);
       }
-      if (j == 0) {
-        pid[a + ck + it] = item.z;
-        pdl[a + ck + it] = (((uint32_t)item.y & 3) == kRem) ? -d : d;
-      }
+      if (j == 0) items[it].w = (((uint32_t)item.y & 3) == kRem) ? -d : d;
+    }
+    __syncthreads();
+    for (int32_t q = threadIdx.x; q < tot; q += 256) {  // the round's pairs, coalesced
+      const int4 item = items[q];
+      pid[a + ck + q] = item.z;
+      pdl[a + ck + q] = item.w;
     }
     ck += tot;
     __syncthreads();
