@@ -216,32 +216,28 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
     if (j == 0) ring[i & (R - 1)] = make_int2(pv, c);
 
     // ---- tops ------------------------------------------------------------------------------
+    // (the common updates below are predicated selects on group-uniform conditions rather
+    // than branches: the four groups of a wave rarely agree, and a divergent branch costs
+    // the CU-shared scalar unit more than the few vector ops it would skip)
     const int32_t k = ks + 1;
-    if (k > lmax) {
-      if (j == G - 1 && lmax - (G - 1) >= 1) topg[a + s0 + (lmax - (G - 1)) - 1] = top;
-      top = Gr::from_prev(top);
-      if (j == 0) top = c;
-      lmax = k;
-      qcnt = 0;
-    } else if (lmax - k < G) {
-      if (j == lmax - k) top = c;
-    } else if (j == 0) {
-      topg[a + s0 + k - 1] = c;
-    }
-    if (k == lmax) {
-      if (j == 0) qn[a + s0 + qcnt] = i;
-      qcnt++;
-    }
+    const bool grow = k > lmax;
+    if (grow && j == G - 1 && lmax - (G - 1) >= 1) topg[a + s0 + (lmax - (G - 1)) - 1] = top;
+    if (!grow && lmax - k >= G && j == 0) topg[a + s0 + k - 1] = c;
+    const int32_t tshift = Gr::from_prev(top);
+    top = grow ? ((j == 0) ? c : tshift) : ((j == lmax - k) ? c : top);
+    qcnt = grow ? 0 : qcnt;
+    lmax = grow ? k : lmax;
+    if (k == lmax && j == 0) qn[a + s0 + qcnt] = i;
+    qcnt += (k == lmax) ? 1 : 0;
 
     // ---- leaves: drop the adopted one, append the new node, sweep ------------------------
-    if (pslot >= 0) {
+    {
       const int32_t nid = Gr::from_next(lid), nlv = Gr::from_next(llv), ncol = Gr::from_next(lcol);
-      if (j >= pslot) {
-        lid = nid;
-        llv = nlv;
-        lcol = ncol;
-      }
-      nl--;
+      const bool drop = pslot >= 0 && j >= pslot;
+      lid = drop ? nid : lid;
+      llv = drop ? nlv : llv;
+      lcol = drop ? ncol : lcol;
+      nl -= (pslot >= 0) ? 1 : 0;
     }
     if (nl == G) {  // leaf list outgrows the group: hand the segment to the next tier
       if (j == 0) ovf[atomicAdd(novf, 1)] = si;
