@@ -428,7 +428,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     if (c->chain_tier <= 0) {
       c->launch(K_CHAIN_G16, k_chain_grp<16>, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, blocks(n, 64)))),
                 dim3(256), s, (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par,
-                d_exta, d_topg, d_qn, d_ovf1, d_cnt + 1, d_err, getenv("CDCX_CXMODE") ? atoi(getenv("CDCX_CXMODE")) : 0);
+                d_exta, d_topg, d_qn, d_ovf1, d_cnt + 1, d_err);
       list = d_ovf1;
       nlist = d_cnt + 1;
       n = c->download(d_cnt + 1, 1, s)[0];
@@ -437,7 +437,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     c->chain_tier_counts[1] = n;
     if (n > 0 && c->chain_tier <= 1) {
       c->launch(K_CHAIN_G64, k_chain_grp<64>, dim3((unsigned)blocks(n, 4)), dim3(256), s, (const Unit*)d_units, d_segs, list,
-                nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par, d_exta, d_topg, d_qn, d_ovf2, d_cnt + 2, d_err, 0);
+                nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par, d_exta, d_topg, d_qn, d_ovf2, d_cnt + 2, d_err);
       list = d_ovf2;
       n = c->download(d_cnt + 2, 1, s)[0];
     }
@@ -622,7 +622,7 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
     std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return units[a].P > units[b].P; });
     int32_t* d_order = c->upload("d_perm_order", order, s);
     c->launch(K_DEC_WIN1, k_dec_perm_grp, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order, NU, d_in,
-              d_idd, d_dld, d_perm, d_cinv, d_nfail, getenv("CDCX_XMODE") ? atoi(getenv("CDCX_XMODE")) : 0);
+              d_idd, d_dld, d_perm, d_cinv, d_nfail);
   }
   int32_t nf = c->dec_tier > 0 ? NU : c->download(d_nfail, 1, s)[0];
   if (nf > 0) {

@@ -49,7 +49,7 @@ __global__ void k_chain_seg(const Unit*, Seg*, int32_t, const int32_t*, const in
                             int32_t*, int32_t*, int32_t*, int2*, const int64_t*, uint32_t*, unsigned long long*);
 template <int G>
 __global__ void k_chain_grp(const Unit*, Seg*, const int32_t*, const int32_t*, const int32_t*, const int32_t*, int32_t*,
-                            int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*, int32_t);
+                            int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*);
 __global__ void k_chain_exits(const Unit*, const Seg*, int32_t, const int32_t*, const int32_t*, const int32_t*, int32_t*,
                               uint32_t*);
 __global__ void k_chain_entries(Unit*, int32_t, Seg*, const int32_t*);
@@ -75,7 +75,7 @@ __global__ void k_dec_sections(const DUnit*, const uint8_t*, uint64_t*, uint64_t
 __global__ void k_dec_perm_lane(const DUnit*, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*, int32_t*,
                                 uint32_t*);
 __global__ void k_dec_perm_grp(DUnit*, const int32_t*, int32_t, const uint8_t*, uint64_t*, uint64_t*, int32_t*, int32_t*,
-                               int32_t*, int32_t);
+                               int32_t*);
 __global__ void k_dec_cinv(const DUnit*, const int32_t*, int32_t*);
 template <int K>
 __global__ void k_dec_perm_window(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);

@@ -84,8 +84,7 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
                                                    const int32_t* __restrict__ cord, const int32_t* __restrict__ inv,
                                                    int32_t* __restrict__ par, int32_t* __restrict__ exta,
                                                    int32_t* __restrict__ topg, int32_t* __restrict__ qn,
-                                                   int32_t* __restrict__ ovf, int32_t* __restrict__ novf, uint32_t* err,
-                                                   int32_t xmode) {
+                                                   int32_t* __restrict__ ovf, int32_t* __restrict__ novf, uint32_t* err) {
   using Gr = Grp<G>;
   using Mask = typename Gr::Mask;
   constexpr int kGroups = 256 / G;
@@ -106,7 +105,7 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
   int32_t lid = 0, llv = 0, lcol = 0, top = 0, cw0 = 0, cw1 = 0, iw0 = 0, iw1 = 0, pval = 0;
 
   auto node = [&](int32_t x) -> int2 {  // {par, column} of row x < i of this segment
-    if (x >= i - R || (xmode & 1)) return ring[x & (R - 1)];
+    if (x >= i - R) return ring[x & (R - 1)];
     return make_int2(par[a + x], cord[a + x]);
   };
 
@@ -281,8 +280,8 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
 }
 
 template __global__ void k_chain_grp<16>(const Unit*, Seg*, const int32_t*, const int32_t*, const int32_t*, const int32_t*,
-                                         int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*, int32_t);
+                                         int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*);
 template __global__ void k_chain_grp<64>(const Unit*, Seg*, const int32_t*, const int32_t*, const int32_t*, const int32_t*,
-                                         int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*, int32_t);
+                                         int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*);
 
 }  // namespace cdcx

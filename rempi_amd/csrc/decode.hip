@@ -444,7 +444,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
                                                      int32_t n_units, const uint8_t* __restrict__ in,
                                                      uint64_t* __restrict__ idd, uint64_t* __restrict__ dld,
                                                      int32_t* __restrict__ perm, int32_t* __restrict__ cinv,
-                                                     int32_t* __restrict__ nfail, int32_t xmode) {
+                                                     int32_t* __restrict__ nfail) {
   constexpr int32_t W = kGW, WM = kGW - 1, MM = kGMap - 1;
   __shared__ int32_t win_all[4][W + 16];      // + one dummy slot per lane
   __shared__ int2 emap_all[4][kGMap + 16];    // {element, absolute position}; + dummies
@@ -480,7 +480,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
   auto slide = [&](bool go) {  // settle [base, base+16), open [base+W, base+W+16) as identity
     const int32_t ph = go ? ((base + j) & WM) : W + j;
     const int32_t v = win[ph];  // (dummy slot when not sliding)
-    if (go && v < M && !(xmode & 2)) {
+    if (go && v < M) {
       pm[v] = base + j;
       ci[base + j] = v;
     }
@@ -538,8 +538,8 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
         emap[sel ? (v & MM) : kGMap + j] = make_int2(v, base + s);
         __builtin_amdgcn_wave_barrier();
       };
-      if (!(xmode & 1)) chunk(0);
-      if (!(xmode & 1) && __builtin_amdgcn_ballot_w64(act && len >= 16))
+      chunk(0);
+      if (__builtin_amdgcn_ballot_w64(act && len >= 16))
         for (int32_t c = 16; __builtin_amdgcn_ballot_w64(act && c <= len); c += 16) chunk(c);
   };
   // 16 pairs at a time: inverse LP of the raw words (x = prefix(prefix(y)) of the
@@ -549,7 +549,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
   int32_t xs = 0, ds = 0;
   auto lp = [&](int32_t k0, int32_t yw_i, int32_t yw_d) {
     const bool inb = k0 + j < P;
-    const int64_t yi = (xmode & 8) ? (k0 + j == 0 ? 1 : 0) : (int64_t)yw_i, yd = (xmode & 8) ? 0 : (int64_t)yw_d;
+    const int64_t yi = (int64_t)yw_i, yd = (int64_t)yw_d;
     const int64_t zi = row_incl_scan64(yi), zd = row_incl_scan64(yd);
     const int64_t xi = cxi + (int64_t)(j + 1) * czi + row_incl_scan64(zi);
     const int64_t xd = cxd + (int64_t)(j + 1) * czd + row_incl_scan64(zd);
@@ -557,7 +557,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
     czd += __shfl(zd, 15, 16);
     cxi = __shfl(xi, 15, 16);
     cxd = __shfl(xd, 15, 16);
-    if (inb && !(xmode & 4)) {
+    if (inb) {
       ip[k0 + j] = (uint64_t)xi;
       dp[k0 + j] = (uint64_t)xd;
     }
