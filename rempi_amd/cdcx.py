@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcdcx.so")
+# CDCX_LIB: another in-tree build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.path.join(HERE, os.environ.get("CDCX_LIB", "libcdcx.so"))
 
 CDCX_OK = 0
 ERRORS = {

@@ -1,0 +1,11 @@
+#!/bin/bash
+# A/B of two in-tree builds on one box: tools/ab.sh <tag> <libA> <libB> [bench args...]
+set -o pipefail
+TAG=$1; A=$2; B=$3; shift 3
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+for i in 1 2; do
+  for L in $A $B; do
+    CDCX_LIB=$L timeout -k 10 300 python -u bench.py --kernel-report "$@" > $OUT/$L.$i.json 2> $OUT/$L.$i.err || { echo "bench $L failed"; tail -20 $OUT/$L.$i.err; exit 1; }
+    echo "$L $i $(python3 -c "import json,sys;print(json.load(open('$OUT/$L.$i.json'))['value'])")"
+  done
+done
