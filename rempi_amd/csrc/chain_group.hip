@@ -135,9 +135,9 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
       cw1 = (s0 + G + j < s1) ? cord[a + s0 + G + j] : 0;
       iw0 = (s0 + j < s1) ? inv[a + s0 + j] : 0;
       iw1 = (s0 + G + j < s1) ? inv[a + s0 + G + j] : 0;
-      continue;
-    }
-    if (i - cb == G) {  // flush this window's parents, slide the cord window
+      // (no `continue`: the first event follows in this iteration; a single loop back-edge
+      // keeps the compiler from copying the whole loop state through extra phi blocks)
+    } else if (i - cb == G) {  // flush this window's parents, slide the cord window
       par[a + cb + j] = pval;
       cb += G;
       cw0 = cw1;
@@ -241,8 +241,8 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
     if (nl == G) {  // leaf list outgrows the group: hand the segment to the next tier
       if (j == 0) ovf[atomicAdd(novf, 1)] = si;
       si = -1;
-      i = s1;
-      continue;
+      i = s1 - 1;  // the rest of this iteration runs on junk state and ends the segment
+      nl = 0;
     }
     if (j == nl) {
       lid = i;

@@ -506,7 +506,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
       const int2 e = emap[act ? (x & MM) : kGMap + j];
       int32_t p = e.y - base;
       int32_t t = p + d;
-      const int32_t bad = act & ((e.x != x) | ((uint32_t)p >= (uint32_t)W) | (t < 0) | (base + t > M - 1) ? 1 : 0);
+      const int32_t bad = act & (((e.x != x) | ((uint32_t)p >= (uint32_t)W) | (t < 0) | (base + t > M - 1)) ? 1 : 0);
       failv |= bad;
       act &= bad ^ 1;
       if (__builtin_amdgcn_ballot_w64(act && t > W - 1)) {
