@@ -354,6 +354,7 @@ def algorithmic_bytes(kernel, n_records, c):
         "k_tile_hist": 32,
         "k_scatter": 32 + 16 + 4,
         "k_unit_prep": 16 + m * (8 + 4),
+        "k_window_rank": m * (8 + 4 + 4 + 8),
         "k_sort_tiles": m * (8 + 8 + 4),
         "k_rank_tiles": m * (8 + 4 + 8 + 4 + 4 + 8),
         "k_epoch": m * 8,

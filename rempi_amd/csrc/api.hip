@@ -24,7 +24,7 @@ namespace {
 
 enum KernelId {
   K_SET_PRESENCE, K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_INC0, K_TILE_SUM, K_RANK_SCAN, K_TILE_P0,
-  K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_G16, K_CHAIN_G64, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
+  K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_WINDOW_RANK, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_G16, K_CHAIN_G64, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
   K_WRITE_UNITS, K_CHUNK_HEADERS, K_FOOTER_ORDER, K_FOOTER_WRITE, K_WRITE_KEYS,
   K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS,
   K_GEN_TILE_SUMS, K_GEN_RANK_SCAN, K_GEN_FRAMES, K_GEN_AKEYS, K_GEN_ARRIVAL, K_GEN_RECORDS,
@@ -32,7 +32,7 @@ enum KernelId {
 };
 const char* kKernelNames[K_COUNT] = {
   "k_set_presence", "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_inc0", "k_tile_sum", "k_rank_scan",
-  "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
+  "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_window_rank", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
   "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
@@ -107,6 +107,8 @@ struct cdcx_ctx {
   // First permutation-rebuild tier (diagnostics / tests): 0 = 16-lane groups, 1 = 256-slot
   // window, 2 = sequential list.
   int dec_tier = getenv("CDCX_DEC_TIER") ? atoi(getenv("CDCX_DEC_TIER")) : 0;
+  // 1: every unit takes the tile sort (skips the windowed rank), for tests
+  int rank_tier = getenv("CDCX_RANK_TIER") ? atoi(getenv("CDCX_RANK_TIER")) : 0;
   int64_t chain_tier_counts[3] = {0, 0, 0};  // segments entering each tier in the last encode
 
   template <class T>
@@ -376,11 +378,17 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int32_t* d_cord = c->buf<int32_t>("cord", N);
   int32_t* d_inv = c->buf<int32_t>("inv", N);
   uint64_t* d_skey = c->buf<uint64_t>("skey", N);
+  // Windowed rank for every unit; units it cannot rank (wfail) take the tile sort.
+  int32_t* d_wfail = c->buf<int32_t>("wfail", NU);
+  HIPCHK(hipMemsetAsync(d_wfail, c->rank_tier > 0 ? 1 : 0, (size_t)NU * 4, s));
+  if (c->rank_tier == 0)
+    c->launch(K_WINDOW_RANK, k_window_rank, dim3(NS), dim3(256), s, (const Unit*)d_units, (const SortTile*)d_st,
+              (const uint64_t*)d_mkey, d_cord, d_inv, d_skey, d_wfail);
   c->launch(K_SORT_TILES, k_sort_tiles, dim3(NS), dim3(256), s, (const Unit*)d_units, (const SortTile*)d_st,
-            (const uint64_t*)d_mkey, d_tkey, d_lrank, d_tmm);
+            (const uint64_t*)d_mkey, d_tkey, d_lrank, d_tmm, (const int32_t*)d_wfail);
   c->launch(K_RANK_TILES, k_rank_tiles, dim3(NS), dim3(256), s, (const Unit*)d_units, (const SortTile*)d_st,
             (const uint64_t*)d_mkey, (const uint64_t*)d_tkey, (const int32_t*)d_lrank, (const uint64_t*)d_tmm, d_cord,
-            d_inv, d_skey);
+            d_inv, d_skey, (const int32_t*)d_wfail);
   uint64_t* d_ep_rank = c->buf<uint64_t>("ep_rank", N);
   uint64_t* d_ep_clk = c->buf<uint64_t>("ep_clk", N);
   c->launch(K_EPOCH, k_epoch<512>, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, d_err);

@@ -370,13 +370,118 @@ __global__ void __launch_bounds__(256) k_unit_prep(Unit* __restrict__ units, con
 }
 
 // ---------------------------------------------------------------------------------------
+// Clock order (format(), :235-239), windowed.  Traces arrive nearly in clock order: an
+// event's rank in its unit differs from its observed index by a few dozen at most.  If every
+// pair q < p with D < p - q <= 2D + 1 has key[q] <= key[p], then (by induction on p - q,
+// stepping D + 1 at a time) every pair more than D apart is in order, so
+//   rank(p) = #{q < p - D} + #{q in [p - D, p + D] ordered before p}
+//           = p - D + (window count, with key 0 standing in for positions before the unit
+//                      and ~0 for those after it)
+// where "ordered before" is (key, index) order.  One pass, no sort: each tile of 1024 events
+// loads its events plus a halo of 2D + 1 before and D after, checks the condition for its
+// events (a key equal to the ~0 sentinel fails it too) and writes cord / inv / skey.  A unit
+// with any failing tile is flagged in wfail and ranked again by the tile sort below.
+__global__ void __launch_bounds__(256) k_window_rank(const Unit* __restrict__ units, const SortTile* __restrict__ st,
+                                                     const uint64_t* __restrict__ mkey, int32_t* __restrict__ cord,
+                                                     int32_t* __restrict__ inv, uint64_t* __restrict__ skey,
+                                                     int32_t* __restrict__ wfail) {
+  constexpr int D = kRankWin;
+  constexpr int H = 2 * D + 1;  // halo before the tile
+  constexpr int NX = H + kSortTile + D;
+  static_assert(D % 4 == 0 && D >= 8, "bulk loops run D - 4 iterations, unrolled by 4");
+  // Key k of the tile's range sits at xk[k + k / 4]: a thread reads keys 4t + x, and the pad
+  // turns its 32 B lane stride into 40 B (10 banks), so 32 lanes read distinct banks.
+  __shared__ uint64_t xk[NX + NX / 4 + 1];
+  __shared__ int32_t rk[kSortTile];
+  const SortTile w = st[blockIdx.x];
+  const Unit u = units[w.unit];
+  const int32_t t0 = w.tile * kSortTile;
+  const int len = min(kSortTile, u.M - t0);
+  for (int k = threadIdx.x; k < NX; k += 256) {
+    const int32_t q = t0 - H + k;
+    xk[k + (k >> 2)] = q < 0 ? 0ull : (q >= u.M ? ~0ull : mkey[u.a + q]);
+  }
+  __syncthreads();
+  const int L = 4 * threadIdx.x;  // own events: tile offsets L..L+3 = keys L + H + j
+  const uint64_t* x0 = xk + 5 * threadIdx.x;
+  auto key = [&](int x) { return x0[x + (x >> 2)]; };  // key L + x (x >= 0)
+  uint64_t own[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) own[j] = key(H + j);
+  // check: event j's window is keys L + j .. L + j + D (positions p - 2D - 1 .. p - D - 1);
+  // x = 3 .. D lies in all four.  (Loops stay rolled: fully unrolled, the compiler keeps
+  // the whole window in registers and the kernel runs at 2 waves/SIMD.)
+  uint64_t mc = max(key(3), key(D));
+#pragma unroll 4
+  for (int x = 4; x < D; x++) mc = max(mc, key(x));
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    uint64_t m = mc;
+#pragma unroll
+    for (int x = j; x < 3; x++) m = max(m, key(x));
+#pragma unroll
+    for (int x = D + 1; x <= D + j; x++) m = max(m, key(x));
+    bad |= (L + j < len) && (m > own[j] || own[j] == ~0ull);
+  }
+  // count: event j's window is keys L + H + j - D .. L + H + j + D; earlier positions count
+  // when key <= own (equal keys keep row order), later ones when key < own.  x = H - D + 3
+  // .. H - 1 is before and inside all four windows, x = H + 4 .. H + D after and inside.
+  int32_t cnt[4] = {0, 0, 0, 0};
+#pragma unroll 4
+  for (int x = H - D + 4; x < H; x++) {
+    const uint64_t v = key(x);
+#pragma unroll
+    for (int j = 0; j < 4; j++) cnt[j] += v <= own[j] ? 1 : 0;
+  }
+#pragma unroll 4
+  for (int x = H + 4; x < H + D; x++) {
+    const uint64_t v = key(x);
+#pragma unroll
+    for (int j = 0; j < 4; j++) cnt[j] += v < own[j] ? 1 : 0;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; e++) {  // key H - D + e: inside the windows of events j <= e
+    const uint64_t v = key(H - D + e);
+#pragma unroll
+    for (int j = 0; j <= e; j++) cnt[j] += v <= own[j] ? 1 : 0;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; e++) {  // the own events among themselves
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (j > e) cnt[j] += own[e] <= own[j] ? 1 : 0;
+      if (j < e) cnt[j] += own[e] < own[j] ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e <= 3; e++) {  // key H + D + e: inside the windows of events j >= e
+    const uint64_t v = key(H + D + e);
+#pragma unroll
+    for (int j = e; j < 4; j++) cnt[j] += v < own[j] ? 1 : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int32_t r = t0 + L + j - D + cnt[j];
+    rk[L + j] = r;
+    if (L + j < len) {
+      inv[u.a + r] = t0 + L + j;
+      skey[u.a + r] = own[j];
+    }
+  }
+  if (__syncthreads_or(bad) && threadIdx.x == 0) wfail[w.unit] = 1;
+  for (int k = threadIdx.x; k < len; k += 256) cord[u.a + t0 + k] = rk[k];
+}
+
+// ---------------------------------------------------------------------------------------
 // Clock order (format(), :235-239).  Sort tiles of <= 1024 matched events in LDS by
 // (key, observed index); then every event's global rank = its rank in its own tile + the
 // number of smaller events in the unit's other tiles (tile min/max prune, binary search
 // where ranges overlap).  Near-sorted traces overlap only with neighbour tiles.
 __global__ void __launch_bounds__(256) k_sort_tiles(const Unit* __restrict__ units, const SortTile* __restrict__ st,
                                                     const uint64_t* __restrict__ mkey, uint64_t* __restrict__ tkey,
-                                                    int32_t* __restrict__ lrank, uint64_t* __restrict__ tminmax) {
+                                                    int32_t* __restrict__ lrank, uint64_t* __restrict__ tminmax,
+                                                    const int32_t* __restrict__ wfail) {
   // Bitonic network held in registers: thread t owns elements 4t..4t+3.  Strides 1 and 2
   // compare inside a thread, strides 4..128 exchange with lane t ^ (stride/4) of the same
   // wave (shuffles), and only strides 256 and 512 (3 of the 55 stages) go through LDS.
@@ -384,6 +489,7 @@ __global__ void __launch_bounds__(256) k_sort_tiles(const Unit* __restrict__ uni
   __shared__ uint64_t xk[kSortTile];
   __shared__ int32_t xi[kSortTile];
   const SortTile w = st[blockIdx.x];
+  if (!wfail[w.unit]) return;  // ranked by k_window_rank
   const Unit u = units[w.unit];
   const int64_t base = u.a + (int64_t)w.tile * kSortTile;
   const int len = min(kSortTile, u.M - w.tile * kSortTile);
@@ -467,7 +573,7 @@ __global__ void __launch_bounds__(256) k_rank_tiles(const Unit* __restrict__ uni
                                                     const uint64_t* __restrict__ mkey, const uint64_t* __restrict__ tkey,
                                                     const int32_t* __restrict__ lrank, const uint64_t* __restrict__ tminmax,
                                                     int32_t* __restrict__ cord, int32_t* __restrict__ inv,
-                                                    uint64_t* __restrict__ skey) {
+                                                    uint64_t* __restrict__ skey, const int32_t* __restrict__ wfail) {
   // Tile-level pruning first: tiles wholly below every key of this tile add their length,
   // tiles wholly above add nothing, and only the overlapping ones (for near-sorted traces
   // the neighbours) are binary-searched per key.
@@ -475,6 +581,7 @@ __global__ void __launch_bounds__(256) k_rank_tiles(const Unit* __restrict__ uni
   __shared__ int32_t ov[kMaxOv];
   __shared__ int32_t nov, below;
   const SortTile w = st[blockIdx.x];
+  if (!wfail[w.unit]) return;  // ranked by k_window_rank
   const Unit u = units[w.unit];
   const int nt = (u.M + kSortTile - 1) / kSortTile;
   const uint64_t* mm = tminmax + 2 * (int64_t)u.sort_tile0;

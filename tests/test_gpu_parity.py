@@ -213,3 +213,37 @@ def test_decode_tiers_vs_oracle(tier, monkeypatch):
             bad.append((t, mode, "records"))
     assert not bad, bad[:5]
     c.close()
+
+
+@pytest.mark.parametrize("tier", [0, 1])
+def test_rank_tiers_vs_oracle(tier, monkeypatch):
+    """Clock-order rank: the windowed pass (tier 0; units it cannot rank take the tile sort)
+    and the tile sort alone (tier 1) give the reference bytes, on multi-tile tables of every
+    arrival mode and on sorted streams with one event moved by about D and 2D (window D = 64),
+    on either side of a tile boundary."""
+    monkeypatch.setenv("CDCX_RANK_TIER", str(tier))
+    c = rempi_amd.Context(131072)
+    monkeypatch.delenv("CDCX_RANK_TIER")
+    rng = np.random.default_rng(505 + tier)
+    bad = []
+    for t in range(30):
+        mode = ["jitter", "jitter", "sorted", "reversed", "random"][t % 5]
+        recs = S.gen_stream(int(rng.integers(1 << 30)), int(rng.integers(1, 6000)), n_sets=int(rng.integers(1, 3)),
+                            n_senders=int(rng.integers(1, 60)), jitter=int(rng.choice([0, 8, 24, 64, 400])), mode=mode)
+        want, _ = O.encode(recs, 131072)
+        got = c.encode_stream(recs)
+        if got != want:
+            bad.append((t, mode, first_diff(got, want)))
+    base = S.gen_stream(99, 3000, n_sets=1, n_senders=16, mode="sorted", p_unmatched=0.0, p_group=0.0)
+    for k in (31, 63, 64, 65, 66, 127, 128, 129, 130, -65, -129):
+        for i in (500, 1000, 1030, 2040):
+            r = list(base)
+            e = r.pop(i)
+            r.insert(min(max(i + k, 0), len(r)), e)
+            recs = S.canonicalize(np.array(r))
+            want, _ = O.encode(recs, 131072)
+            got = c.encode_stream(recs)
+            if got != want:
+                bad.append(("move", i, k, first_diff(got, want)))
+    assert not bad, bad[:5]
+    c.close()
