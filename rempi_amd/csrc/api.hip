@@ -363,40 +363,54 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   c->check_err(d_err, s);
   units = c->download(d_units, NU, s);
 
-  // Sort tiles.
+  // Clock-order rank: the windowed pass for every unit (tiles of kSortTile events); the units
+  // it flags (wfail) are ranked again by the tile sort after the next download, then get
+  // their epoch line and cuts (both skip flagged units until then).
   std::vector<SortTile> st;
   for (int32_t u = 0; u < NU; u++) {
     units[u].sort_tile0 = (int32_t)st.size();
+    units[u].wfail = c->rank_tier > 0 ? 1 : 0;
     for (int32_t q = 0; q * kSortTile < units[u].M; q++) st.push_back(SortTile{u, q});
   }
   const int64_t NS = (int64_t)st.size();
   d_units = c->upload("units", units, s);
   SortTile* d_st = c->upload("sort_tiles", st, s);
-  uint64_t* d_tkey = c->buf<uint64_t>("tkey", N);
-  int32_t* d_lrank = c->buf<int32_t>("lrank", N);
-  uint64_t* d_tmm = c->buf<uint64_t>("tminmax", 2 * NS);
   int32_t* d_cord = c->buf<int32_t>("cord", N);
   int32_t* d_inv = c->buf<int32_t>("inv", N);
   uint64_t* d_skey = c->buf<uint64_t>("skey", N);
-  // Windowed rank for every unit; units it cannot rank (wfail) take the tile sort.
-  int32_t* d_wfail = c->buf<int32_t>("wfail", NU);
-  HIPCHK(hipMemsetAsync(d_wfail, c->rank_tier > 0 ? 1 : 0, (size_t)NU * 4, s));
   if (c->rank_tier == 0)
-    c->launch(K_WINDOW_RANK, k_window_rank, dim3(NS), dim3(256), s, (const Unit*)d_units, (const SortTile*)d_st,
-              (const uint64_t*)d_mkey, d_cord, d_inv, d_skey, d_wfail);
-  c->launch(K_SORT_TILES, k_sort_tiles, dim3(NS), dim3(256), s, (const Unit*)d_units, (const SortTile*)d_st,
-            (const uint64_t*)d_mkey, d_tkey, d_lrank, d_tmm, (const int32_t*)d_wfail);
-  c->launch(K_RANK_TILES, k_rank_tiles, dim3(NS), dim3(256), s, (const Unit*)d_units, (const SortTile*)d_st,
-            (const uint64_t*)d_mkey, (const uint64_t*)d_tkey, (const int32_t*)d_lrank, (const uint64_t*)d_tmm, d_cord,
-            d_inv, d_skey, (const int32_t*)d_wfail);
+    c->launch(K_WINDOW_RANK, k_window_rank, dim3(NS), dim3(256), s, d_units, (const SortTile*)d_st,
+              (const uint64_t*)d_mkey, d_cord, d_inv, d_skey);
   uint64_t* d_ep_rank = c->buf<uint64_t>("ep_rank", N);
   uint64_t* d_ep_clk = c->buf<uint64_t>("ep_clk", N);
-  c->launch(K_EPOCH, k_epoch<512>, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, d_err);
-  // Chain: closed-prefix segments simulated independently, then stitched (chain.hip).
   int32_t* d_segend = c->buf<int32_t>("segend", N);
-  c->launch(K_CUTS, k_cuts, dim3(NU), dim3(256), s, d_units, (const int32_t*)d_cord, d_segend);
-  c->check_err(d_err, s);
-  units = c->download(d_units, NU, s);
+  auto epoch_cuts = [&]() {
+    c->launch(K_EPOCH, k_epoch<512>, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, d_err);
+    // Chain: closed-prefix segments simulated independently, then stitched (chain.hip).
+    c->launch(K_CUTS, k_cuts, dim3(NU), dim3(256), s, d_units, (const int32_t*)d_cord, d_segend);
+    c->check_err(d_err, s);
+    units = c->download(d_units, NU, s);
+  };
+  epoch_cuts();
+  std::vector<SortTile> fst;
+  for (int32_t u = 0; u < NU; u++)
+    if (units[u].wfail)
+      for (int32_t q = 0; q * kSortTile < units[u].M; q++) fst.push_back(SortTile{u, q});
+  if (!fst.empty()) {
+    SortTile* d_fst = c->upload("sort_tiles_fb", fst, s);
+    uint64_t* d_tkey = c->buf<uint64_t>("tkey", N);
+    int32_t* d_lrank = c->buf<int32_t>("lrank", N);
+    uint64_t* d_tmm = c->buf<uint64_t>("tminmax", 2 * NS);
+    c->launch(K_SORT_TILES, k_sort_tiles, dim3((unsigned)fst.size()), dim3(256), s, (const Unit*)d_units,
+              (const SortTile*)d_fst, (const uint64_t*)d_mkey, d_tkey, d_lrank, d_tmm);
+    c->launch(K_RANK_TILES, k_rank_tiles, dim3((unsigned)fst.size()), dim3(256), s, (const Unit*)d_units,
+              (const SortTile*)d_fst, (const uint64_t*)d_mkey, (const uint64_t*)d_tkey, (const int32_t*)d_lrank,
+              (const uint64_t*)d_tmm, d_cord, d_inv, d_skey);
+    for (Unit& u : units) u.wfail = u.wfail ? 0 : 2;  // epoch and cuts for the re-ranked units only
+    d_units = c->upload("units", units, s);
+    epoch_cuts();
+  }
+  for (Unit& u : units) u.wfail = 0;
   int64_t nsegs = 0;
   for (Unit& u : units) {
     u.seg0 = (int32_t)nsegs;

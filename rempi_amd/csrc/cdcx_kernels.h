@@ -33,10 +33,10 @@ __global__ void k_chunks(const int32_t*, const int64_t*, const int64_t*, const i
 __global__ void k_units_lb(const Chunk*, int32_t, const int64_t*, const int32_t*, const int32_t*, const int64_t*,
                            const int32_t*, int2*);
 __global__ void k_unit_prep(Unit*, const TRec*, uint64_t*, int32_t*, int32_t*, int32_t*, uint64_t*, uint32_t*);
-__global__ void k_window_rank(const Unit*, const SortTile*, const uint64_t*, int32_t*, int32_t*, uint64_t*, int32_t*);
-__global__ void k_sort_tiles(const Unit*, const SortTile*, const uint64_t*, uint64_t*, int32_t*, uint64_t*, const int32_t*);
+__global__ void k_window_rank(Unit*, const SortTile*, const uint64_t*, int32_t*, int32_t*, uint64_t*);
+__global__ void k_sort_tiles(const Unit*, const SortTile*, const uint64_t*, uint64_t*, int32_t*, uint64_t*);
 __global__ void k_rank_tiles(const Unit*, const SortTile*, const uint64_t*, const uint64_t*, const int32_t*,
-                             const uint64_t*, int32_t*, int32_t*, uint64_t*, const int32_t*);
+                             const uint64_t*, int32_t*, int32_t*, uint64_t*);
 template <int HCAP>
 __global__ void k_epoch(Unit*, const uint64_t*, uint64_t*, uint64_t*, uint32_t*);
 // chain.hip

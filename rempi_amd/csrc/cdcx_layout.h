@@ -60,6 +60,7 @@ struct Unit {
   int32_t sort_tile0;     // first global sort tile of the unit
   int32_t nseg;           // closed-prefix segments of the clock-order permutation
   int32_t seg0;           // first global segment index
+  int32_t wfail;          // k_window_rank could not rank it (1); epoch/cuts skip units != 0
   int64_t out_off;        // byte offset of the unit in the batch output
   int64_t key_off;        // offset of its sorted keys in the batch key list
 };

@@ -35,6 +35,7 @@ __global__ void __launch_bounds__(256) k_cuts(Unit* __restrict__ units, const in
                                               int32_t* __restrict__ segend) {
   __shared__ int32_t lds[4];
   Unit& u = units[blockIdx.x];
+  if (u.wfail != 0) return;  // not ranked yet (k_window_rank), or already done
   const int64_t a = u.a;
   const int32_t M = u.M;
   int32_t cmax = -1, cn = 0;

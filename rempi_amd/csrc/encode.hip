@@ -380,11 +380,11 @@ __global__ void __launch_bounds__(256) k_unit_prep(Unit* __restrict__ units, con
 // where "ordered before" is (key, index) order.  One pass, no sort: each tile of 1024 events
 // loads its events plus a halo of 2D + 1 before and D after, checks the condition for its
 // events (a key equal to the ~0 sentinel fails it too) and writes cord / inv / skey.  A unit
-// with any failing tile is flagged in wfail and ranked again by the tile sort below.
-__global__ void __launch_bounds__(256) k_window_rank(const Unit* __restrict__ units, const SortTile* __restrict__ st,
+// with any failing tile is flagged (Unit::wfail); the host ranks it again with the tile sort
+// below, launched over the flagged units' tiles only.
+__global__ void __launch_bounds__(256) k_window_rank(Unit* __restrict__ units, const SortTile* __restrict__ st,
                                                      const uint64_t* __restrict__ mkey, int32_t* __restrict__ cord,
-                                                     int32_t* __restrict__ inv, uint64_t* __restrict__ skey,
-                                                     int32_t* __restrict__ wfail) {
+                                                     int32_t* __restrict__ inv, uint64_t* __restrict__ skey) {
   constexpr int D = kRankWin;
   constexpr int H = 2 * D + 1;  // halo before the tile
   constexpr int NX = H + kSortTile + D;
@@ -469,7 +469,7 @@ __global__ void __launch_bounds__(256) k_window_rank(const Unit* __restrict__ un
       skey[u.a + r] = own[j];
     }
   }
-  if (__syncthreads_or(bad) && threadIdx.x == 0) wfail[w.unit] = 1;
+  if (__syncthreads_or(bad) && threadIdx.x == 0) units[w.unit].wfail = 1;
   for (int k = threadIdx.x; k < len; k += 256) cord[u.a + t0 + k] = rk[k];
 }
 
@@ -480,8 +480,7 @@ __global__ void __launch_bounds__(256) k_window_rank(const Unit* __restrict__ un
 // where ranges overlap).  Near-sorted traces overlap only with neighbour tiles.
 __global__ void __launch_bounds__(256) k_sort_tiles(const Unit* __restrict__ units, const SortTile* __restrict__ st,
                                                     const uint64_t* __restrict__ mkey, uint64_t* __restrict__ tkey,
-                                                    int32_t* __restrict__ lrank, uint64_t* __restrict__ tminmax,
-                                                    const int32_t* __restrict__ wfail) {
+                                                    int32_t* __restrict__ lrank, uint64_t* __restrict__ tminmax) {
   // Bitonic network held in registers: thread t owns elements 4t..4t+3.  Strides 1 and 2
   // compare inside a thread, strides 4..128 exchange with lane t ^ (stride/4) of the same
   // wave (shuffles), and only strides 256 and 512 (3 of the 55 stages) go through LDS.
@@ -489,7 +488,6 @@ __global__ void __launch_bounds__(256) k_sort_tiles(const Unit* __restrict__ uni
   __shared__ uint64_t xk[kSortTile];
   __shared__ int32_t xi[kSortTile];
   const SortTile w = st[blockIdx.x];
-  if (!wfail[w.unit]) return;  // ranked by k_window_rank
   const Unit u = units[w.unit];
   const int64_t base = u.a + (int64_t)w.tile * kSortTile;
   const int len = min(kSortTile, u.M - w.tile * kSortTile);
@@ -573,7 +571,7 @@ __global__ void __launch_bounds__(256) k_rank_tiles(const Unit* __restrict__ uni
                                                     const uint64_t* __restrict__ mkey, const uint64_t* __restrict__ tkey,
                                                     const int32_t* __restrict__ lrank, const uint64_t* __restrict__ tminmax,
                                                     int32_t* __restrict__ cord, int32_t* __restrict__ inv,
-                                                    uint64_t* __restrict__ skey, const int32_t* __restrict__ wfail) {
+                                                    uint64_t* __restrict__ skey) {
   // Tile-level pruning first: tiles wholly below every key of this tile add their length,
   // tiles wholly above add nothing, and only the overlapping ones (for near-sorted traces
   // the neighbours) are binary-searched per key.
@@ -581,7 +579,6 @@ __global__ void __launch_bounds__(256) k_rank_tiles(const Unit* __restrict__ uni
   __shared__ int32_t ov[kMaxOv];
   __shared__ int32_t nov, below;
   const SortTile w = st[blockIdx.x];
-  if (!wfail[w.unit]) return;  // ranked by k_window_rank
   const Unit u = units[w.unit];
   const int nt = (u.M + kSortTile - 1) / kSortTile;
   const uint64_t* mm = tminmax + 2 * (int64_t)u.sort_tile0;
@@ -696,6 +693,7 @@ __global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const u
   __shared__ int32_t nlist;
   // After compaction the hash arrays are reused as the sort buffers and emulator storage.
   Unit& u = units[blockIdx.x];
+  if (u.wfail != 0) return;  // not ranked yet (k_window_rank), or already done
   if (kBig && u.S != -1) return;
   const int64_t a = u.a;
   const int32_t M = u.M;
