@@ -938,12 +938,14 @@ __global__ void __launch_bounds__(256) k_pos_cols(const Unit* __restrict__ units
 // list when it moves -- IGNOREs, REMOVEs whose element is still pending (its ADD comes
 // later), ADDs whose element has already moved (its REMOVE came earlier).  Negative when the
 // second occurrence is the REMOVE.  The pair index is a running count of second occurrences.
-__global__ void __launch_bounds__(256) k_deltas(const Unit* __restrict__ units, const uint32_t* __restrict__ seq,
-                                                const int32_t* __restrict__ sx, int32_t* __restrict__ pid,
-                                                int32_t* __restrict__ pdl) {
+__global__ void __launch_bounds__(256, 8) k_deltas(const Unit* __restrict__ units, const uint32_t* __restrict__ seq,
+                                                   const int32_t* __restrict__ sx, int32_t* __restrict__ pid,
+                                                   int32_t* __restrict__ pdl) {
+  // LDS and registers are kept small (16 KB, <= 64 VGPRs) so that 8 blocks share a CU: the
+  // kernel waits on LDS and barriers, and occupancy is what hides that.
   __shared__ int32_t lds[4];
-  __shared__ int4 items[1024];  // second occurrences of the round: {position s, entry, id}
-  constexpr int32_t RING = 4096;  // the last RING sequence entries, for the span counts
+  __shared__ int2 items[1024];    // second occurrences of the round: {position s, entry}, then {s, delta}
+  constexpr int32_t RING = 2048;  // the last RING sequence entries, for the span counts
   __shared__ uint32_t ring[RING];
   const Unit u = units[blockIdx.x];
   const int64_t a = u.a;
@@ -952,15 +954,13 @@ __global__ void __launch_bounds__(256) k_deltas(const Unit* __restrict__ units, 
   const int g = threadIdx.x >> 4, j = threadIdx.x & 15, gw = (threadIdx.x >> 4) & 3;
   const int32_t* sxa = sx + 2 * a;
   int32_t ck = 0;
-  // this round's sequence entries and ids; the next round's are loaded while the spans of
-  // this one are counted
+  // this round's sequence entries; the next round's are loaded while the spans of this one
+  // are counted
   uint32_t e[4];
-  int32_t xs[4];
 #pragma unroll
   for (int q = 0; q < 4; q++) {
     const int32_t z = 4 * threadIdx.x + q;
     e[q] = (z < L) ? sq[z] : kIgn;
-    xs[q] = (z < L) ? sxa[z] : 0;
   }
   for (int32_t b = 0; b < L; b += 1024) {
     const int32_t q0 = b + 4 * threadIdx.x;
@@ -973,25 +973,24 @@ __global__ void __launch_bounds__(256) k_deltas(const Unit* __restrict__ units, 
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       ring[(q0 + q) & (RING - 1)] = e[q];
-      if ((e[q] & 3) != kIgn && (int32_t)(e[q] >> 2) < q0 + q) items[k++] = make_int4(q0 + q, (int32_t)e[q], xs[q], 0);
+      if ((e[q] & 3) != kIgn && (int32_t)(e[q] >> 2) < q0 + q) items[k++] = make_int2(q0 + q, (int32_t)e[q]);
     }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int32_t z = q0 + 1024 + q;
       e[q] = (z < L) ? sq[z] : kIgn;
-      xs[q] = (z < L) ? sxa[z] : 0;
     }
     const int32_t rlo = b + 1024 - RING;  // entries >= rlo are in the ring
     // one item per 16-lane group: the group counts its span 16 entries at a time
     for (int32_t it = g; it < tot; it += 16) {
-      const int4 item = items[it];
+      const int2 item = items[it];
       const int32_t s = item.x, f = (int32_t)((uint32_t)item.y >> 2);
       int32_t d = 0;
       for (int32_t z0 = f + 1; z0 < s; z0 += 16) {
         const int32_t z = z0 + j;
         uint32_t y = ring[z & (RING - 1)];
-        // entries older than the ring (spans longer than ~3 K) come from memory, behind a
+        // entries older than the ring (spans longer than ~1 K) come from memory, behind a
         // wave-uniform branch so that the common case issues no global load at all
         if (__builtin_amdgcn_ballot_w64(z < s && z < rlo))
           if (z < s && z < rlo) y = sq[z];
@@ -1000,13 +999,13 @@ __global__ void __launch_bounds__(256) k_deltas(const Unit* __restrict__ units, 
         const bool c = (z < s) & ((yt == kIgn) | ((yt == kRem) & (pt > s)) | ((yt == kAdd) & (pt < s)));
         d += __popc((uint32_t)(__ballot(c) >> (16 * gw)) & 0xFFFFu);
       }
-      if (j == 0) items[it].w = (((uint32_t)item.y & 3) == kRem) ? -d : d;
+      if (j == 0) items[it].y = (((uint32_t)item.y & 3) == kRem) ? -d : d;
     }
     __syncthreads();
     for (int32_t q = threadIdx.x; q < tot; q += 256) {  // the round's pairs, coalesced
-      const int4 item = items[q];
-      pid[a + ck + q] = item.z;
-      pdl[a + ck + q] = item.w;
+      const int2 item = items[q];
+      pid[a + ck + q] = sxa[item.x];
+      pdl[a + ck + q] = item.y;
     }
     ck += tot;
     __syncthreads();
