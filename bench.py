@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--world", type=int, default=1024, help="ranks in the traced job")
     ap.add_argument("--events", type=int, default=10_000_000, help="events per rank trace")
-    ap.add_argument("--ranks-per-gpu", type=int, default=64, help="rank traces resident per GPU (one step)")
+    ap.add_argument("--ranks-per-gpu", type=int, default=96, help="rank traces resident per GPU (one step)")
     ap.add_argument("--jitter", type=int, default=8)
     ap.add_argument("--max-len", type=int, default=131072, help="REMPI_MAX")
     ap.add_argument("--verify-ranks", type=int, default=1, help="ranks checked byte-exact vs the CPU oracle")
@@ -323,7 +323,7 @@ def main():
                        "ranks_per_gpu": B, "events_per_rank": args.events, "records_per_step_per_gpu": n_records,
                        "jitter": args.jitter, "rempi_max": args.max_len, "streams_per_gpu": S,
                        "compressed_bytes_per_event": round(comp_per_event, 3),
-                       "hbm_used_gb": round((total_b - free_b) / 1e9, 1),
+                       "hbm_used_gb": round((total_b - free_b) / 1e9, 1), "hbm_total_gb": round(total_b / 1e9, 1),
                        "parallelism": f"dp{ws} (independent rank traces per GPU)",
                        "verify_failures": int(counters[2])},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
