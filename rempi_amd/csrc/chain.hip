@@ -39,17 +39,37 @@ __global__ void __launch_bounds__(256) k_cuts(Unit* __restrict__ units, const in
   const int64_t a = u.a;
   const int32_t M = u.M;
   int32_t cmax = -1, cn = 0;
-  for (int32_t b = 0; b < M; b += 256) {
-    const int32_t r = b + threadIdx.x;
-    const bool valid = r < M;
-    const int32_t v = valid ? cord[a + r] : -1;
+  // 4 rows per thread per round; the next round's columns are loaded during this one
+  int32_t vn[4];
+  auto load = [&](int32_t r0) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) vn[q] = (r0 + q < M) ? cord[a + r0 + q] : -1;
+  };
+  load(4 * threadIdx.x);
+  for (int32_t b = 0; b < M; b += 1024) {
+    const int32_t r0 = b + 4 * threadIdx.x;
+    int32_t v[4], lm = -1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      v[q] = vn[q];
+      lm = max(lm, v[q]);
+    }
+    load(r0 + 1024);
     int32_t tmax;
-    const int32_t ex = block_exclusive_scan<256>(v, -1, OpMax(), lds, &tmax);
-    const int32_t inc = max(max(ex, cmax), v);
-    const bool cut = valid && inc == r;
+    int32_t run = max(block_exclusive_scan<256>(lm, -1, OpMax(), lds, &tmax), cmax);
+    bool cut[4];
+    int32_t nc = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      run = max(run, v[q]);
+      cut[q] = r0 + q < M && run == r0 + q;
+      nc += cut[q] ? 1 : 0;
+    }
     int32_t tc;
-    const int32_t pos = block_exclusive_scan<256>((int32_t)cut, 0, OpAdd(), lds, &tc);
-    if (cut) segend[a + cn + pos] = r;
+    int32_t pos = cn + block_exclusive_scan<256>(nc, 0, OpAdd(), lds, &tc);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (cut[q]) segend[a + pos++] = r0 + q;
     cn += tc;
     cmax = max(cmax, tmax);
   }
