@@ -327,7 +327,8 @@ def main():
                        "parallelism": f"dp{ws} (independent rank traces per GPU)",
                        "verify_failures": int(counters[2])},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": pmc_traffic(dom, per_launch_records), "traffic_source": PMC_TRAFFIC,
                          "launch_ms": round(dom_ms / dom_launches, 3),
                          "algorithmic_bytes_per_launch": round(algo),
                          "pipeline_achieved": round(pipeline_bytes(comp_per_event) * total_records / tmax / 1e9, 2)},
@@ -370,6 +371,21 @@ def algorithmic_bytes(kernel, n_records, c):
         "k_dec_records": c + m * (4 + 8 + 8 + 1) + 32,
     }.get(kernel, 32)
     return per * n_records
+
+
+PMC_TRAFFIC = "profiles/r01/pmc_traffic.json"
+
+
+def pmc_traffic(kernel, n_records):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+    (tools/pmc_traffic.py: read bytes = 2 x FETCH_SIZE per the gfx950 correction, checked on
+    k_tile_hist), scaled to the records one launch processes; None if not collected."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), PMC_TRAFFIC)
+    try:
+        k = json.load(open(path))["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None
+    return None if k is None else round(k["bytes_per_record"] * n_records)
 
 
 def pipeline_bytes(c):
