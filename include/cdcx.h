@@ -72,6 +72,19 @@ const char* cdcx_kernel_name(int k);
 int cdcx_encode_stream(cdcx_ctx* ctx, const int32_t* rec8, size_t n_rec, uint8_t** out,
                        size_t* out_len);
 
+/* Basic -> CDC transcoder.  A REMPI_ENCODE=0 record file holds one
+ * rank's canonical event stream as [size_t len][len bytes of 8 x int32 events] chunks
+ * (rempi_encoder_basic::write_record_file, rempi_encoder_basic.cpp:205-224; read back by
+ * :238-321), so its CDC image is cdcx_encode_stream of the concatenated chunks.  The n_files
+ * rank files are encoded as one device batch; outs[i] (cdcx_free) receives file i's
+ * complete rank_<r>.rempi image (out_lens[i] bytes).  CDCX_ERR_ARG for a truncated file, a
+ * chunk that is not a whole number of records, or a record whose type is not
+ * REMPI_MPI_EVENT_TYPE_TEST (2): basic files may hold MPI_Recv events, which the CDC
+ * recorder never records.  REMPI_GZIP=1 basic files are zlib streams: inflate them on the
+ * host first. */
+int cdcx_transcode_basic(cdcx_ctx* ctx, size_t n_files, const uint8_t* const* files, const size_t* lens,
+                         uint8_t** outs, size_t* out_lens);
+
 /* Host buffers: encode exactly one chunk (the records of one
  * extract_encoder_input_format_chunk call).  *payload (cdcx_free) is what
  * write_record_file emits after the size_t length; *epoch_ranks (cdcx_free, may be NULL

@@ -11,6 +11,11 @@
 //        (rempi_io_thread.cpp:56-97) is replayed: extract_encoder_input_format_chunk ->
 //        encode -> write_record_file, then close_record_file (footer,
 //        rempi_encoder_cdc.cpp:2085-2135).  Prints "encode_s <seconds>".
+//   ref_cdc encode_basic <in.rec> <out.basic> <REMPI_MAX> [gzip]
+//        the same push, then the REMPI_ENCODE=0 record loop with rempi_encoder_basic
+//        (rempi_encoder_basic.cpp:81-224): a sequence of [size_t len][len bytes of 8 x int32
+//        events] chunks (with `gzip`, REMPI_GZIP=1: each payload a zlib stream).  These files
+//        are what the basic -> CDC transcoder reads (§8(f)).
 //   ref_cdc decode <in.rempi> <out.tables>
 //        read_record_file + decode per chunk (rempi_encoder_cdc.cpp:933-1299), dumping the
 //        decoded tables (int64 little-endian, layout in oracle/tables_format.md).
@@ -77,6 +82,38 @@ int do_encode(const char* in, const char* out, int max_len) {
   return 0;
 }
 
+int do_encode_basic(const char* in, const char* out, int max_len, int gzip) {
+  FILE* f = fopen(in, "rb");
+  if (!f) { perror(in); return 2; }
+  std::vector<int32_t> buf;
+  int32_t r[8];
+  while (fread(r, sizeof r, 1, f) == 1) buf.insert(buf.end(), r, r + 8);
+  fclose(f);
+  size_t n = buf.size() / 8;
+
+  rempi_mode = 0;
+  rempi_gzip = gzip;
+  rempi_max_event_length = max_len;
+  rempi_event_list<rempi_event*> events((size_t)1 << 40, 100);
+  for (size_t i = 0; i < n; i++) {
+    const int32_t* q = &buf[8 * i];
+    events.push(rempi_event::create_test_event(q[0], q[2], q[3], q[4], q[5], q[6], q[7]));
+  }
+  events.push_all();
+
+  rempi_encoder_basic enc(0, out);
+  enc.open_record_file(out);
+  while (true) {
+    rempi_encoder_input_format* fmt = enc.create_encoder_input_format();
+    if (!enc.extract_encoder_input_format_chunk(events, fmt)) { delete fmt; break; }
+    enc.encode();
+    enc.write_record_file();
+  }
+  enc.close_record_file();
+  printf("encode_basic records %zu\n", n);
+  return 0;
+}
+
 // rempi_encoder_cdc::decode keeps replay-engine state across chunks and aborts on the
 // second chunk whenever #tables != #epoch ranks (rempi_encoder_cdc.cpp:1262-1267); that
 // state is not part of the decoded data, so the harness clears it before each chunk.
@@ -131,7 +168,11 @@ int do_decode(const char* in, const char* out) {
 
 int main(int argc, char** argv) {
   if (argc >= 5 && std::string(argv[1]) == "encode") return do_encode(argv[2], argv[3], atoi(argv[4]));
+  if (argc >= 5 && std::string(argv[1]) == "encode_basic")
+    return do_encode_basic(argv[2], argv[3], atoi(argv[4]), argc >= 6 && std::string(argv[5]) == "gzip");
   if (argc >= 4 && std::string(argv[1]) == "decode") return do_decode(argv[2], argv[3]);
-  fprintf(stderr, "usage: ref_cdc encode <in.rec> <out.rempi> <REMPI_MAX> | decode <in.rempi> <out.tables>\n");
+  fprintf(stderr,
+          "usage: ref_cdc encode <in.rec> <out.rempi> <REMPI_MAX> | encode_basic <in.rec> <out.basic> <REMPI_MAX> [gzip] |"
+          " decode <in.rempi> <out.tables>\n");
   return 1;
 }

@@ -54,6 +54,7 @@ _SIGNATURES = {
     "cdcx_kernel_count": ([], ctypes.c_int),
     "cdcx_kernel_name": ([ctypes.c_int], ctypes.c_char_p),
     "cdcx_encode_stream": ([_vp, _i32p, ctypes.c_size_t, P(_u8p), P(ctypes.c_size_t)], ctypes.c_int),
+    "cdcx_transcode_basic": ([_vp, ctypes.c_size_t, P(_u8p), P(ctypes.c_size_t), P(_u8p), P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_encode_chunk": ([_vp, _i32p, ctypes.c_size_t, P(_u8p), P(ctypes.c_size_t), P(_i32p), P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_encode_batch_device": ([_vp, ctypes.c_int32, _vp, _i64p, P(_vp), _i64p, _i64p, _vp], ctypes.c_int),
     "cdcx_batch_sorted_keys": ([_vp, P(_vp), _i64p], ctypes.c_int),
@@ -149,6 +150,24 @@ class Context:
         data = ctypes.string_at(out, n.value)
         L.cdcx_free(out)
         return data
+
+    def transcode_basic(self, files):
+        """REMPI_ENCODE=0 record files (bytes each, one rank per file) -> their CDC rank files,
+        encoded as one device batch (cdcx_transcode_basic)."""
+        L = lib()
+        files = [bytes(f) for f in files]
+        n = len(files)
+        bufs = [np.frombuffer(f, dtype=np.uint8) if f else np.zeros(1, np.uint8) for f in files]
+        ptrs = (_u8p * max(n, 1))(*[b.ctypes.data_as(_u8p) for b in bufs])
+        lens = (ctypes.c_size_t * max(n, 1))(*[len(f) for f in files])
+        outs = (_u8p * max(n, 1))()
+        olens = (ctypes.c_size_t * max(n, 1))()
+        self._check(L.cdcx_transcode_basic(self._c, n, ptrs, lens, outs, olens), "transcode_basic")
+        res = []
+        for i in range(n):
+            res.append(ctypes.string_at(outs[i], olens[i]))
+            L.cdcx_free(outs[i])
+        return res
 
     def encode_chunk(self, recs: np.ndarray):
         L = lib()

@@ -824,6 +824,64 @@ int cdcx_encode_stream(cdcx_ctx* c, const int32_t* rec8, size_t n, uint8_t** out
   });
 }
 
+int cdcx_transcode_basic(cdcx_ctx* c, size_t nf, const uint8_t* const* files, const size_t* lens, uint8_t** outs,
+                         size_t* out_lens) {
+  if (!c || (nf && (!files || !lens || !outs || !out_lens)) || nf > (size_t)INT32_MAX) return CDCX_ERR_ARG;
+  for (size_t f = 0; f < nf; f++) {
+    outs[f] = nullptr;
+    out_lens[f] = 0;
+  }
+  return guarded(c, [&] {
+    // framing (rempi_encoder_basic.cpp:238-321): chunks of whole 32 B TEST records
+    struct Span {
+      const uint8_t* p;
+      size_t n;
+    };
+    std::vector<Span> spans;
+    std::vector<int64_t> ro(nf + 1, 0);
+    for (size_t f = 0; f < nf; f++) {
+      const uint8_t* b = files[f];
+      size_t p = 0, recs = 0;
+      if (lens[f] && !b) throw CdcxError{CDCX_ERR_ARG, "null basic file"};
+      while (p < lens[f]) {
+        if (lens[f] - p < 8) throw CdcxError{CDCX_ERR_ARG, "truncated basic record file"};
+        uint64_t n;
+        memcpy(&n, b + p, 8);
+        p += 8;
+        if (n % 32 || n > lens[f] - p) throw CdcxError{CDCX_ERR_ARG, "basic chunk is not a whole number of records"};
+        for (uint64_t k = 0; k < n; k += 32) {
+          int32_t type;
+          memcpy(&type, b + p + k + 4, 4);
+          if (type != 2) throw CdcxError{CDCX_ERR_ARG, "basic record is not a test event (type 2)"};
+        }
+        if (n) spans.push_back(Span{b + p, (size_t)n});
+        recs += n / 32;
+        p += n;
+      }
+      ro[f + 1] = ro[f] + (int64_t)recs;
+    }
+    hipStream_t s = c->stream;
+    int32_t* d = c->buf<int32_t>("h_in", 8 * ro[nf]);
+    size_t off = 0;
+    for (const Span& sp : spans) {
+      HIPCHK(hipMemcpyAsync(reinterpret_cast<uint8_t*>(d) + off, sp.p, sp.n, hipMemcpyHostToDevice, s));
+      off += sp.n;
+    }
+    std::vector<int64_t> fo, fl;
+    encode_batch(c, (int32_t)nf, d, ro.data(), fo, fl, s);
+    std::vector<std::vector<uint8_t>> h(nf);
+    for (size_t f = 0; f < nf; f++) {
+      h[f].resize(fl[f]);
+      HIPCHK(hipMemcpyAsync(h[f].data(), c->d_out + fo[f], fl[f], hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    for (size_t f = 0; f < nf; f++) {
+      outs[f] = host_copy(h[f]);
+      out_lens[f] = h[f].size();
+    }
+  });
+}
+
 int cdcx_encode_chunk(cdcx_ctx* c, const int32_t* rec8, size_t n, uint8_t** payload, size_t* payload_len,
                       int32_t** epoch_ranks, size_t* n_epoch_ranks) {
   if (!c || (n && !rec8) || !payload || !payload_len || !epoch_ranks || !n_epoch_ranks) return CDCX_ERR_ARG;

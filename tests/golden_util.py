@@ -26,3 +26,18 @@ def load(name):
 
 def all_files():
     return glob.glob(os.path.join(GOLDEN, "*.npz"))
+
+
+def basic_names():
+    """Fixtures of the basic -> CDC transcoder (tests/golden/make_basic_golden.py)."""
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "basic_*.npz")))
+
+
+def load_basic(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    d["max_len"] = int(d["max_len"])
+    d["basic"] = d["basic"].tobytes()
+    d["basic_gz"] = d["basic_gz"].tobytes()
+    d["rempi"] = d["rempi"].tobytes()
+    return d

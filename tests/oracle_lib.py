@@ -197,6 +197,33 @@ def ref_encode(recs: np.ndarray, max_len: int = 131072):
             return f.read(), secs
 
 
+def ref_encode_basic(recs: np.ndarray, max_len: int = 131072, gzip: bool = False) -> bytes:
+    """Run the reference REMPI_ENCODE=0 encoder (rempi_encoder_basic, via oracle/_ref/ref_cdc
+    encode_basic) -> the basic record file: [size_t len][len bytes of 8 x int32] chunks
+    (gzip: REMPI_GZIP=1, each chunk payload a zlib stream)."""
+    with tempfile.TemporaryDirectory() as d:
+        inp, outp = os.path.join(d, "in.rec"), os.path.join(d, "out.basic")
+        np.ascontiguousarray(recs, dtype=np.int32).tofile(inp)
+        res = subprocess.run([REF_BIN, "encode_basic", inp, outp, str(max_len)] + (["gzip"] if gzip else []),
+                             capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"ref encode_basic failed rc={res.returncode}: {res.stderr[-500:]}")
+        with open(outp, "rb") as f:
+            return f.read()
+
+
+def parse_basic(data: bytes) -> np.ndarray:
+    """Records of a basic record file (rempi_encoder_basic.cpp:238-321 read loop): the chunks'
+    8 x int32 events concatenated."""
+    out, p = [], 0
+    while p < len(data):
+        n = int(np.frombuffer(data[p:p + 8], np.uint64)[0])
+        p += 8
+        out.append(np.frombuffer(data[p:p + n], np.int32).reshape(-1, 8))
+        p += n
+    return np.concatenate(out) if out else np.zeros((0, 8), np.int32)
+
+
 def ref_decode(data: bytes):
     with tempfile.TemporaryDirectory() as d:
         inp, outp = os.path.join(d, "in.rempi"), os.path.join(d, "out.tables")
