@@ -42,7 +42,10 @@ extern "C" {
 
 typedef struct cdcx_opts {
   int64_t max_event_length; /* REMPI_MAX (rempi_config.cpp:103-108); default 131072 */
-  int32_t gzip;             /* REMPI_GZIP; must be 0 (zlib stage is not on the device path) */
+  int32_t gzip;             /* REMPI_GZIP (0 or 1): the host-buffer entry points (encode/decode/
+                               reconstruct stream, encode chunk, transcode) apply the zlib stage
+                               on the host; the device-resident batch entry points carry plain
+                               CDC and return CDCX_ERR_ARG on a gzip context */
   int32_t device;           /* HIP device ordinal */
   int64_t reserved[4];
 } cdcx_opts;
@@ -71,6 +74,15 @@ const char* cdcx_kernel_name(int k);
  * rank_<r>.rempi image (chunks, separator, footer). */
 int cdcx_encode_stream(cdcx_ctx* ctx, const int32_t* rec8, size_t n_rec, uint8_t** out,
                        size_t* out_len);
+
+/* REMPI_GZIP=1 stage of a whole rank file, on the host: every chunk
+ * payload replaced by its zlib stream (rempi_encoder_cdc::write_record_file,
+ * rempi_encoder_cdc.cpp:804-844, deflate at Z_DEFAULT_COMPRESSION as in
+ * rempi_compression_util.cpp:233-325) or back (read_record_file, :960-978); the separator
+ * and footer are kept.  No context or GPU needed.  *out is freed with cdcx_free.
+ * CDCX_ERR_CORRUPT for bad framing or a bad zlib stream. */
+int cdcx_gzip_file(const uint8_t* in, size_t len, uint8_t** out, size_t* out_len);
+int cdcx_gunzip_file(const uint8_t* in, size_t len, uint8_t** out, size_t* out_len);
 
 /* Basic -> CDC transcoder.  A REMPI_ENCODE=0 record file holds one
  * rank's canonical event stream as [size_t len][len bytes of 8 x int32 events] chunks

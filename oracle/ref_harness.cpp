@@ -4,7 +4,7 @@
 // the C++ restatement (oracle/cdc_oracle.cpp) and the HIP path can be pinned to
 // bytes produced by the reference itself.
 //
-//   ref_cdc encode <in.rec> <out.rempi> <REMPI_MAX>
+//   ref_cdc encode <in.rec> <out.rempi> <REMPI_MAX> [gzip]
 //        in.rec = n x 8 x int32 canonical records (rempi_event.h:40-48 layout).
 //        Each record is pushed through rempi_event_list::push (rempi_event_list.cpp:66-99,
 //        run-length merge), then the record loop of rempi_io_thread::write_record
@@ -16,7 +16,8 @@
 //        (rempi_encoder_basic.cpp:81-224): a sequence of [size_t len][len bytes of 8 x int32
 //        events] chunks (with `gzip`, REMPI_GZIP=1: each payload a zlib stream).  These files
 //        are what the basic -> CDC transcoder reads (§8(f)).
-//   ref_cdc decode <in.rempi> <out.tables>
+//   ref_cdc decode <in.rempi> <out.tables> [gzip]
+//        (`gzip`: REMPI_GZIP=1, chunk payloads are zlib streams)
 //        read_record_file + decode per chunk (rempi_encoder_cdc.cpp:933-1299), dumping the
 //        decoded tables (int64 little-endian, layout in oracle/tables_format.md).
 //        Prints "decode_s <seconds>".
@@ -46,7 +47,7 @@ struct Dump {
   }
 };
 
-int do_encode(const char* in, const char* out, int max_len) {
+int do_encode(const char* in, const char* out, int max_len, int gzip) {
   FILE* f = fopen(in, "rb");
   if (!f) { perror(in); return 2; }
   std::vector<int32_t> buf;
@@ -56,7 +57,7 @@ int do_encode(const char* in, const char* out, int max_len) {
   size_t n = buf.size() / 8;
 
   rempi_mode = 0;
-  rempi_gzip = 0;
+  rempi_gzip = gzip;
   rempi_max_event_length = max_len;
   rempi_event_list<rempi_event*> events((size_t)1 << 40, 100);
   for (size_t i = 0; i < n; i++) {
@@ -122,9 +123,9 @@ struct Dec : rempi_encoder_cdc {
   void reset_replay_state() { solid_mc_next_clocks_umap_umap.clear(); }
 };
 
-int do_decode(const char* in, const char* out) {
+int do_decode(const char* in, const char* out, int gzip) {
   rempi_mode = 1;
-  rempi_gzip = 0;
+  rempi_gzip = gzip;
   Dec dec(in);
   dec.open_record_file();
   FILE* f = fopen(out, "wb");
@@ -167,12 +168,14 @@ int do_decode(const char* in, const char* out) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  if (argc >= 5 && std::string(argv[1]) == "encode") return do_encode(argv[2], argv[3], atoi(argv[4]));
+  if (argc >= 5 && std::string(argv[1]) == "encode")
+    return do_encode(argv[2], argv[3], atoi(argv[4]), argc >= 6 && std::string(argv[5]) == "gzip");
   if (argc >= 5 && std::string(argv[1]) == "encode_basic")
     return do_encode_basic(argv[2], argv[3], atoi(argv[4]), argc >= 6 && std::string(argv[5]) == "gzip");
-  if (argc >= 4 && std::string(argv[1]) == "decode") return do_decode(argv[2], argv[3]);
+  if (argc >= 4 && std::string(argv[1]) == "decode")
+    return do_decode(argv[2], argv[3], argc >= 5 && std::string(argv[4]) == "gzip");
   fprintf(stderr,
-          "usage: ref_cdc encode <in.rec> <out.rempi> <REMPI_MAX> | encode_basic <in.rec> <out.basic> <REMPI_MAX> [gzip] |"
-          " decode <in.rempi> <out.tables>\n");
+          "usage: ref_cdc encode <in.rec> <out.rempi> <REMPI_MAX> [gzip] | encode_basic <in.rec> <out.basic> <REMPI_MAX> [gzip] |"
+          " decode <in.rempi> <out.tables> [gzip]\n");
   return 1;
 }

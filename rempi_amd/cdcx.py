@@ -54,6 +54,8 @@ _SIGNATURES = {
     "cdcx_kernel_count": ([], ctypes.c_int),
     "cdcx_kernel_name": ([ctypes.c_int], ctypes.c_char_p),
     "cdcx_encode_stream": ([_vp, _i32p, ctypes.c_size_t, P(_u8p), P(ctypes.c_size_t)], ctypes.c_int),
+    "cdcx_gzip_file": ([_u8p, ctypes.c_size_t, P(_u8p), P(ctypes.c_size_t)], ctypes.c_int),
+    "cdcx_gunzip_file": ([_u8p, ctypes.c_size_t, P(_u8p), P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_transcode_basic": ([_vp, ctypes.c_size_t, P(_u8p), P(ctypes.c_size_t), P(_u8p), P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_encode_chunk": ([_vp, _i32p, ctypes.c_size_t, P(_u8p), P(ctypes.c_size_t), P(_i32p), P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_encode_batch_device": ([_vp, ctypes.c_int32, _vp, _i64p, P(_vp), _i64p, _i64p, _vp], ctypes.c_int),
@@ -113,12 +115,36 @@ def generate_host(params: GenParams, rank: int) -> np.ndarray:
     return arr
 
 
+def _zlib_stage(fn, data: bytes) -> bytes:
+    L = lib()
+    buf = np.frombuffer(bytes(data), dtype=np.uint8) if data else np.zeros(1, np.uint8)
+    out = _u8p()
+    n = ctypes.c_size_t()
+    rc = fn(buf.ctypes.data_as(_u8p), len(data), ctypes.byref(out), ctypes.byref(n))
+    if rc != 0:
+        raise CdcxError(rc, "zlib stage")
+    res = ctypes.string_at(out, n.value)
+    L.cdcx_free(out)
+    return res
+
+
+def gzip_file(data: bytes) -> bytes:
+    """A plain CDC rank file -> its REMPI_GZIP=1 form (cdcx_gzip_file; host only, no GPU)."""
+    return _zlib_stage(lib().cdcx_gzip_file, data)
+
+
+def gunzip_file(data: bytes) -> bytes:
+    """A REMPI_GZIP=1 CDC rank file -> the plain one (cdcx_gunzip_file; host only, no GPU)."""
+    return _zlib_stage(lib().cdcx_gunzip_file, data)
+
+
 class Context:
     """One codec context on one HIP device (cdcx_create / cdcx_destroy)."""
 
-    def __init__(self, max_event_length: int = 131072, device: int = 0):
+    def __init__(self, max_event_length: int = 131072, device: int = 0, gzip: int = 0):
+        """gzip=1 is REMPI_GZIP=1: the host-buffer calls apply the zlib stage on the host."""
         L = lib()
-        opts = _Opts(max_event_length, 0, device, (ctypes.c_int64 * 4)())
+        opts = _Opts(max_event_length, gzip, device, (ctypes.c_int64 * 4)())
         self._c = L.cdcx_create(ctypes.byref(opts))
         if not self._c:
             raise CdcxError(5, f"cdcx_create failed (device {device})")

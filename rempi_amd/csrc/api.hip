@@ -16,6 +16,7 @@
 
 #include "../../include/cdcx.h"
 #include "cdcx_kernels.h"
+#include "gzip_stage.h"
 #include "hash_order.h"
 
 using namespace cdcx;
@@ -74,6 +75,7 @@ constexpr const char* kAliasWnf = "chain";    // with_next flags       <- chain 
 
 struct cdcx_ctx {
   int device = 0;
+  int gzip = 0;  // REMPI_GZIP: host-buffer encode/decode apply the zlib stage (gzip_stage.hip)
   int64_t max_len = 131072;
   std::string err;
   std::map<std::string, DevBuf> bufs;
@@ -230,6 +232,9 @@ int guarded(cdcx_ctx* c, F&& f) {
   } catch (const std::bad_alloc&) {
     c->err = "host allocation failed";
     return CDCX_ERR_NOMEM;
+  } catch (const GzipError& e) {
+    c->err = std::string("zlib stage: ") + e.msg;
+    return CDCX_ERR_CORRUPT;
   }
 }
 
@@ -756,10 +761,11 @@ cdcx_ctx* cdcx_create(const cdcx_opts* opts) {
   if (opts) {
     c->device = opts->device;
     if (opts->max_event_length > 0) c->max_len = opts->max_event_length;
-    if (opts->gzip != 0) {
+    if (opts->gzip != 0 && opts->gzip != 1) {
       delete c;
       return nullptr;
     }
+    c->gzip = opts->gzip;
   }
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || c->device < 0 || c->device >= n || hipSetDevice(c->device) != hipSuccess) {
@@ -790,7 +796,7 @@ const char* cdcx_kernel_name(int k) { return (k >= 0 && k < K_COUNT) ? kKernelNa
 
 int cdcx_encode_batch_device(cdcx_ctx* c, int32_t n_ranks, const int32_t* d_rec, const int64_t* rec_off,
                              const uint8_t** d_out, int64_t* out_off, int64_t* out_len, void* stream) {
-  if (!c || n_ranks <= 0 || !rec_off || !d_out || !out_off || !out_len) return CDCX_ERR_ARG;
+  if (!c || n_ranks <= 0 || !rec_off || !d_out || !out_off || !out_len || c->gzip) return CDCX_ERR_ARG;
   return guarded(c, [&] {
     std::vector<int64_t> fo, fl;
     encode_batch(c, n_ranks, d_rec, rec_off, fo, fl, (hipStream_t)stream);
@@ -819,6 +825,7 @@ int cdcx_encode_stream(cdcx_ctx* c, const int32_t* rec8, size_t n, uint8_t** out
     std::vector<uint8_t> h(fl[0]);
     HIPCHK(hipMemcpyAsync(h.data(), c->d_out + fo[0], fl[0], hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    if (c->gzip) h = gzip_file(h.data(), h.size());
     *out = host_copy(h);
     *out_len = h.size();
   });
@@ -876,6 +883,7 @@ int cdcx_transcode_basic(cdcx_ctx* c, size_t nf, const uint8_t* const* files, co
     }
     HIPCHK(hipStreamSynchronize(s));
     for (size_t f = 0; f < nf; f++) {
+      if (c->gzip) h[f] = gzip_file(h[f].data(), h[f].size());
       outs[f] = host_copy(h[f]);
       out_lens[f] = h[f].size();
     }
@@ -931,6 +939,7 @@ int cdcx_encode_chunk(cdcx_ctx* c, const int32_t* rec8, size_t n, uint8_t** payl
         q = p;
       }
     }
+    if (c->gzip && !pl.empty()) pl = deflate_payload(pl.data(), pl.size());
     *payload = host_copy(pl);
     *payload_len = pl.size();
     *epoch_ranks = host_copy(er);
@@ -943,6 +952,12 @@ int cdcx_encode_chunk(cdcx_ctx* c, const int32_t* rec8, size_t n, uint8_t** payl
 int cdcx_decode_stream(cdcx_ctx* c, const uint8_t* in, size_t len, uint8_t** dump, size_t* dump_len) {
   if (!c || (len && !in) || !dump || !dump_len) return CDCX_ERR_ARG;
   return guarded(c, [&] {
+    std::vector<uint8_t> plain;
+    if (c->gzip) {
+      plain = gunzip_file(in, len);
+      in = plain.data();
+      len = plain.size();
+    }
     hipStream_t s = c->stream;
     uint8_t* d = c->buf<uint8_t>("h_file", len);
     if (len) HIPCHK(hipMemcpyAsync(d, in, len, hipMemcpyHostToDevice, s));
@@ -957,6 +972,12 @@ int cdcx_reconstruct_stream(cdcx_ctx* c, const uint8_t* in, size_t len, const in
                             int32_t** rec8, size_t* n_out) {
   if (!c || (len && !in) || (n_keys && !keys) || !rec8 || !n_out) return CDCX_ERR_ARG;
   return guarded(c, [&] {
+    std::vector<uint8_t> plain;
+    if (c->gzip) {
+      plain = gunzip_file(in, len);
+      in = plain.data();
+      len = plain.size();
+    }
     hipStream_t s = c->stream;
     uint8_t* d = c->buf<uint8_t>("h_file", len);
     if (len) HIPCHK(hipMemcpyAsync(d, in, len, hipMemcpyHostToDevice, s));
@@ -969,10 +990,39 @@ int cdcx_reconstruct_stream(cdcx_ctx* c, const uint8_t* in, size_t len, const in
   });
 }
 
+int cdcx_gzip_file(const uint8_t* in, size_t len, uint8_t** out, size_t* out_len) {
+  if ((len && !in) || !out || !out_len) return CDCX_ERR_ARG;
+  try {
+    std::vector<uint8_t> v = gzip_file(in, len);
+    *out = host_copy(v);
+    *out_len = v.size();
+    return CDCX_OK;
+  } catch (const GzipError&) {
+    return CDCX_ERR_CORRUPT;
+  } catch (const std::bad_alloc&) {
+    return CDCX_ERR_NOMEM;
+  }
+}
+
+int cdcx_gunzip_file(const uint8_t* in, size_t len, uint8_t** out, size_t* out_len) {
+  if ((len && !in) || !out || !out_len) return CDCX_ERR_ARG;
+  try {
+    std::vector<uint8_t> v = gunzip_file(in, len);
+    *out = host_copy(v);
+    *out_len = v.size();
+    return CDCX_OK;
+  } catch (const GzipError&) {
+    return CDCX_ERR_CORRUPT;
+  } catch (const std::bad_alloc&) {
+    return CDCX_ERR_NOMEM;
+  }
+}
+
 int cdcx_decode_batch_device(cdcx_ctx* c, int32_t n_ranks, const uint8_t* d_in, const int64_t* in_off,
                              const int64_t* in_len, const int32_t* d_keys, int64_t n_keys, const int32_t** d_rec_out,
                              int64_t* n_rec_out, const int32_t** d_perm, void* stream) {
-  if (!c || n_ranks <= 0 || !d_in || !in_off || !in_len || !d_rec_out || !n_rec_out || !d_perm) return CDCX_ERR_ARG;
+  if (!c || n_ranks <= 0 || !d_in || !in_off || !in_len || !d_rec_out || !n_rec_out || !d_perm || c->gzip)
+    return CDCX_ERR_ARG;
   return guarded(c, [&] {
     std::vector<int64_t> off(in_off, in_off + n_ranks), len(in_len, in_len + n_ranks);
     decode_batch(c, n_ranks, d_in, off, len, reinterpret_cast<const int2*>(d_keys), n_keys, d_keys != nullptr,

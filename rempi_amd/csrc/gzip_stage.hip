@@ -1,0 +1,145 @@
+// gzip_stage.hip -- the REMPI_GZIP=1 stage of a CDC rank file, on the host.
+//
+// With REMPI_GZIP=1 the reference writes each chunk as [size_t compressed size][one zlib stream
+// of the chunk payload] (rempi_encoder_cdc::write_record_file, rempi_encoder_cdc.cpp:804-844;
+// the stream is deflateInit(Z_DEFAULT_COMPRESSION) over the chunk's write queue with
+// Z_NO_FLUSH between pieces and Z_FINISH at the end, rempi_compression_util.cpp:233-325), and
+// reads it back by inflating (:960-978).  The separator (size_t 0) and the footer (:2085-2135)
+// are written as they are.  Deflate's output does not depend on how its input is split into
+// pieces, so one deflate call per chunk payload gives the reference's bytes (with the same
+// zlib; both use the system libz of the image).  The deflate output cannot be made on the GPU
+// and still match zlib byte for byte, so this stage stays on the host; chunks are
+// independent and are compressed on several threads.
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "gzip_stage.h"
+
+namespace cdcx {
+
+namespace {
+
+struct Piece {
+  size_t off, len;  // payload in the input
+};
+
+// Chunk payloads of a framed rank file: [size_t n][n bytes]... until the separator (0);
+// *rest = offset of the separator (len when the file has none).
+std::vector<Piece> chunks_of(const uint8_t* in, size_t len, size_t* rest) {
+  std::vector<Piece> v;
+  size_t p = 0;
+  while (p < len) {
+    if (len - p < 8) throw GzipError{"truncated chunk length"};
+    uint64_t n;
+    memcpy(&n, in + p, 8);
+    if (n == 0) break;  // all_epoch_rank_separator: the footer follows
+    if (n > len - p - 8) throw GzipError{"chunk runs past the end of the file"};
+    v.push_back(Piece{p + 8, (size_t)n});
+    p += 8 + n;
+  }
+  *rest = p;
+  return v;
+}
+
+template <class F>
+void parallel_for(size_t n, F&& f) {
+  const size_t nt = std::min<size_t>(n, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+  if (nt <= 1) {
+    for (size_t i = 0; i < n; i++) f(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> th;
+  std::vector<std::exception_ptr> err(nt);
+  for (size_t t = 0; t < nt; t++)
+    th.emplace_back([&, t] {
+      try {
+        for (size_t i; (i = next++) < n;) f(i);
+      } catch (...) {
+        err[t] = std::current_exception();
+      }
+    });
+  for (auto& x : th) x.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+}
+
+std::vector<uint8_t> frame(const std::vector<std::vector<uint8_t>>& z, const uint8_t* in, size_t rest, size_t len) {
+  size_t total = len - rest;
+  for (auto& b : z) total += 8 + b.size();
+  std::vector<uint8_t> out;
+  out.reserve(total);
+  for (auto& b : z) {
+    const uint64_t n = b.size();
+    out.insert(out.end(), reinterpret_cast<const uint8_t*>(&n), reinterpret_cast<const uint8_t*>(&n) + 8);
+    out.insert(out.end(), b.begin(), b.end());
+  }
+  out.insert(out.end(), in + rest, in + len);
+  return out;
+}
+
+}  // namespace
+
+std::vector<uint8_t> deflate_payload(const uint8_t* p, size_t n) {
+  z_stream s{};
+  if (deflateInit(&s, Z_DEFAULT_COMPRESSION) != Z_OK) throw GzipError{"deflateInit failed"};
+  std::vector<uint8_t> out(deflateBound(&s, (uLong)n));
+  s.next_in = const_cast<Bytef*>(p);
+  s.avail_in = (uInt)n;
+  s.next_out = out.data();
+  s.avail_out = (uInt)out.size();
+  const int rc = deflate(&s, Z_FINISH);
+  out.resize(out.size() - s.avail_out);
+  deflateEnd(&s);
+  if (rc != Z_STREAM_END) throw GzipError{"deflate did not finish"};
+  return out;
+}
+
+std::vector<uint8_t> inflate_payload(const uint8_t* p, size_t n) {
+  z_stream s{};
+  if (inflateInit(&s) != Z_OK) throw GzipError{"inflateInit failed"};
+  std::vector<uint8_t> out(std::max<size_t>(4 * n, 4096));
+  s.next_in = const_cast<Bytef*>(p);
+  s.avail_in = (uInt)n;
+  int rc;
+  while (true) {
+    s.next_out = out.data() + s.total_out;
+    s.avail_out = (uInt)(out.size() - s.total_out);
+    rc = inflate(&s, Z_NO_FLUSH);
+    if (rc == Z_STREAM_END) break;
+    if (rc != Z_OK && rc != Z_BUF_ERROR) break;
+    if (s.avail_out == 0) {
+      out.resize(out.size() * 2);
+    } else if (s.avail_in == 0) {
+      rc = Z_DATA_ERROR;  // input ended inside the stream
+      break;
+    }
+  }
+  out.resize(s.total_out);
+  inflateEnd(&s);
+  if (rc != Z_STREAM_END) throw GzipError{"corrupt zlib chunk"};
+  return out;
+}
+
+std::vector<uint8_t> gzip_file(const uint8_t* in, size_t len) {
+  size_t rest;
+  const std::vector<Piece> pc = chunks_of(in, len, &rest);
+  std::vector<std::vector<uint8_t>> z(pc.size());
+  parallel_for(pc.size(), [&](size_t i) { z[i] = deflate_payload(in + pc[i].off, pc[i].len); });
+  return frame(z, in, rest, len);
+}
+
+std::vector<uint8_t> gunzip_file(const uint8_t* in, size_t len) {
+  size_t rest;
+  const std::vector<Piece> pc = chunks_of(in, len, &rest);
+  std::vector<std::vector<uint8_t>> z(pc.size());
+  parallel_for(pc.size(), [&](size_t i) { z[i] = inflate_payload(in + pc[i].off, pc[i].len); });
+  return frame(z, in, rest, len);
+}
+
+}  // namespace cdcx

@@ -7,7 +7,8 @@ stream, so its CDC image (what a REMPI_ENCODE=7 recording of the same run writes
 CDC encode of the concatenated chunks (cdcx_transcode_basic).  Output files keep the input
 names (both encoders write REMPI_DIR/rank_<r>.rempi) under OUTDIR.  Files are encoded in
 device batches of --batch ranks.  REMPI_GZIP=1 basic files are zlib streams; they are
-inflated on the host first (--gzip).
+inflated on the host first (--gzip).  --gzip-out writes REMPI_GZIP=1 CDC files (host zlib
+stage, cdcx_gzip_file).
 """
 from __future__ import annotations
 
@@ -38,9 +39,10 @@ def main(argv=None) -> int:
     ap.add_argument("--max-len", type=int, default=131072, help="REMPI_MAX of the CDC recording")
     ap.add_argument("--batch", type=int, default=16, help="rank files per device batch")
     ap.add_argument("--gzip", action="store_true", help="inputs were written with REMPI_GZIP=1")
+    ap.add_argument("--gzip-out", action="store_true", help="write REMPI_GZIP=1 CDC files")
     args = ap.parse_args(argv)
     os.makedirs(args.out, exist_ok=True)
-    ctx = Context(args.max_len)
+    ctx = Context(args.max_len, gzip=1 if args.gzip_out else 0)
     tin = tout = 0
     for i in range(0, len(args.files), args.batch):
         paths = args.files[i:i + args.batch]

@@ -41,3 +41,17 @@ def load_basic(name):
     d["basic_gz"] = d["basic_gz"].tobytes()
     d["rempi"] = d["rempi"].tobytes()
     return d
+
+
+def gzip_names():
+    """Fixtures of the REMPI_GZIP=1 stage (tests/golden/make_gzip_golden.py)."""
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "gzip_*.npz")))
+
+
+def load_gzip(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    d["max_len"] = int(d["max_len"])
+    for k in ("rempi", "rempi_gz", "tables"):
+        d[k] = d[k].tobytes()
+    return d

@@ -184,12 +184,13 @@ def have_ref() -> bool:
     return os.path.exists(REF_BIN)
 
 
-def ref_encode(recs: np.ndarray, max_len: int = 131072):
-    """Run the reference encoder (oracle/_ref/ref_cdc) -> (bytes, seconds)."""
+def ref_encode(recs: np.ndarray, max_len: int = 131072, gzip: bool = False):
+    """Run the reference encoder (oracle/_ref/ref_cdc) -> (bytes, seconds); gzip: REMPI_GZIP=1."""
     with tempfile.TemporaryDirectory() as d:
         inp, outp = os.path.join(d, "in.rec"), os.path.join(d, "out.rempi")
         np.ascontiguousarray(recs, dtype=np.int32).tofile(inp)
-        res = subprocess.run([REF_BIN, "encode", inp, outp, str(max_len)], capture_output=True, text=True)
+        res = subprocess.run([REF_BIN, "encode", inp, outp, str(max_len)] + (["gzip"] if gzip else []),
+                             capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"ref encode failed rc={res.returncode}: {res.stderr[-500:]}")
         secs = float(res.stdout.split()[1])
@@ -224,12 +225,12 @@ def parse_basic(data: bytes) -> np.ndarray:
     return np.concatenate(out) if out else np.zeros((0, 8), np.int32)
 
 
-def ref_decode(data: bytes):
+def ref_decode(data: bytes, gzip: bool = False):
     with tempfile.TemporaryDirectory() as d:
         inp, outp = os.path.join(d, "in.rempi"), os.path.join(d, "out.tables")
         with open(inp, "wb") as f:
             f.write(data)
-        res = subprocess.run([REF_BIN, "decode", inp, outp], capture_output=True, text=True)
+        res = subprocess.run([REF_BIN, "decode", inp, outp] + (["gzip"] if gzip else []), capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"ref decode failed rc={res.returncode}: {res.stderr[-500:]}")
         secs = float(res.stdout.split()[1])
