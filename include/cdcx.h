@@ -47,7 +47,11 @@ typedef struct cdcx_opts {
                                on the host; the device-resident batch entry points carry plain
                                CDC and return CDCX_ERR_ARG on a gzip context */
   int32_t device;           /* HIP device ordinal */
-  int64_t reserved[4];
+  int32_t encode;           /* REMPI_ENCODE (rempi_config.h:46-48): 0 or 4 = CDC; 7 = rep
+                               (rempi_encoder_rep.cpp:50-146: every table keeps its set id,
+                               count and epoch line, all other sections empty) */
+  int32_t pad;
+  int64_t reserved[3];
 } cdcx_opts;
 
 typedef struct cdcx_ctx cdcx_ctx;

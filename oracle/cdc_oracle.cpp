@@ -178,6 +178,7 @@ struct Table {
 
 struct Encoder {
   int64_t max_len;
+  int rep = 0;  // REMPI_ENCODE=7 (rempi_encoder_rep.cpp:50-146): epoch lines only
   std::unordered_set<int> footer_ranks;  // rempi_encoder_cdc.cpp:60, :266
   Sink out;
 
@@ -254,6 +255,12 @@ struct Encoder {
       body.put_u64(8 * ep_rank.size());
       body.put(ep_rank.data(), 8 * ep_rank.size());
       body.put(ep_clock.data(), 8 * ep_clock.size());
+      if (rep) {
+        // rempi_encoder_rep::compress_non_matched_events (:88-133): wp length/size, mi
+        // length/size, uid size, ucnt size all 0; compress_matched_events (:137-145): pair size 0.
+        for (int k = 0; k < 7; k++) body.put_u64(0);
+        continue;
+      }
       std::vector<u64> wp = t.with_prev;
       lp_forward(wp);
       body.put_u64(wp.size());
@@ -474,9 +481,15 @@ extern "C" {
 
 int oracle_encode(const int32_t* rec, size_t n, int64_t max_len, uint8_t** out, size_t* out_len,
                   size_t* footer_off) {
+  return oracle_encode_ex(rec, n, max_len, 0, out, out_len, footer_off);
+}
+
+int oracle_encode_ex(const int32_t* rec, size_t n, int64_t max_len, int rep, uint8_t** out, size_t* out_len,
+                     size_t* footer_off) {
   if (!out || !out_len || (n && !rec)) return ORACLE_ERR_ARG;
   Encoder e;
   e.max_len = max_len;
+  e.rep = rep;
   size_t pos = 0;
   // run() inline so the footer offset can be reported.
   while (pos < n) {

@@ -31,6 +31,10 @@ extern "C" {
  * chunks, the size_t 0 separator and the footer.  *out is malloc'ed. */
 int oracle_encode(const int32_t* rec, size_t n, int64_t max_len, uint8_t** out, size_t* out_len,
                   size_t* footer_off);
+/* Same, with rep != 0 selecting the REMPI_ENCODE=7 encoder (rempi_encoder_rep.cpp:50-146):
+ * every table keeps set id, count and epoch line; all later sections are empty. */
+int oracle_encode_ex(const int32_t* rec, size_t n, int64_t max_len, int rep, uint8_t** out, size_t* out_len,
+                     size_t* footer_off);
 
 /* Decode a whole rank_<r>.rempi byte image into the int64 table dump described in
  * oracle/tables_format.md (the same dump oracle/_ref/ref_cdc writes). *out is malloc'ed. */

@@ -4,7 +4,8 @@
 // the C++ restatement (oracle/cdc_oracle.cpp) and the HIP path can be pinned to
 // bytes produced by the reference itself.
 //
-//   ref_cdc encode <in.rec> <out.rempi> <REMPI_MAX> [gzip]
+//   ref_cdc encode <in.rec> <out.rempi> <REMPI_MAX> [gzip|rep]
+//        (`rep`: the REMPI_ENCODE=7 encoder, rempi_encoder_rep: epoch lines only)
 //        in.rec = n x 8 x int32 canonical records (rempi_event.h:40-48 layout).
 //        Each record is pushed through rempi_event_list::push (rempi_event_list.cpp:66-99,
 //        run-length merge), then the record loop of rempi_io_thread::write_record
@@ -47,7 +48,7 @@ struct Dump {
   }
 };
 
-int do_encode(const char* in, const char* out, int max_len, int gzip) {
+int do_encode(const char* in, const char* out, int max_len, int gzip, int rep) {
   FILE* f = fopen(in, "rb");
   if (!f) { perror(in); return 2; }
   std::vector<int32_t> buf;
@@ -67,7 +68,9 @@ int do_encode(const char* in, const char* out, int max_len, int gzip) {
   }
   events.push_all();
 
-  rempi_encoder_cdc enc(0, out);
+  rempi_encoder_cdc cdc(0, out);
+  rempi_encoder_rep repe(0, out);
+  rempi_encoder_cdc& enc = rep ? repe : cdc;
   enc.open_record_file();
   double t0 = now_s();
   while (true) {
@@ -169,13 +172,14 @@ int do_decode(const char* in, const char* out, int gzip) {
 
 int main(int argc, char** argv) {
   if (argc >= 5 && std::string(argv[1]) == "encode")
-    return do_encode(argv[2], argv[3], atoi(argv[4]), argc >= 6 && std::string(argv[5]) == "gzip");
+    return do_encode(argv[2], argv[3], atoi(argv[4]), argc >= 6 && std::string(argv[5]) == "gzip",
+                     argc >= 6 && std::string(argv[5]) == "rep");
   if (argc >= 5 && std::string(argv[1]) == "encode_basic")
     return do_encode_basic(argv[2], argv[3], atoi(argv[4]), argc >= 6 && std::string(argv[5]) == "gzip");
   if (argc >= 4 && std::string(argv[1]) == "decode")
     return do_decode(argv[2], argv[3], argc >= 5 && std::string(argv[4]) == "gzip");
   fprintf(stderr,
-          "usage: ref_cdc encode <in.rec> <out.rempi> <REMPI_MAX> [gzip] | encode_basic <in.rec> <out.basic> <REMPI_MAX> [gzip] |"
+          "usage: ref_cdc encode <in.rec> <out.rempi> <REMPI_MAX> [gzip|rep] | encode_basic <in.rec> <out.basic> <REMPI_MAX> [gzip] |"
           " decode <in.rempi> <out.tables> [gzip]\n");
   return 1;
 }

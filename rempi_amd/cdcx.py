@@ -35,7 +35,7 @@ class CdcxError(RuntimeError):
 
 class _Opts(ctypes.Structure):
     _fields_ = [("max_event_length", ctypes.c_int64), ("gzip", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("reserved", ctypes.c_int64 * 4)]
+                ("encode", ctypes.c_int32), ("pad", ctypes.c_int32), ("reserved", ctypes.c_int64 * 3)]
 
 
 class GenParams(ctypes.Structure):
@@ -141,10 +141,11 @@ def gunzip_file(data: bytes) -> bytes:
 class Context:
     """One codec context on one HIP device (cdcx_create / cdcx_destroy)."""
 
-    def __init__(self, max_event_length: int = 131072, device: int = 0, gzip: int = 0):
-        """gzip=1 is REMPI_GZIP=1: the host-buffer calls apply the zlib stage on the host."""
+    def __init__(self, max_event_length: int = 131072, device: int = 0, gzip: int = 0, encode: int = 4):
+        """gzip=1 is REMPI_GZIP=1: the host-buffer calls apply the zlib stage on the host.
+        encode is REMPI_ENCODE: 4 = CDC, 7 = rep (epoch lines only)."""
         L = lib()
-        opts = _Opts(max_event_length, gzip, device, (ctypes.c_int64 * 4)())
+        opts = _Opts(max_event_length, gzip, device, encode, 0, (ctypes.c_int64 * 3)())
         self._c = L.cdcx_create(ctypes.byref(opts))
         if not self._c:
             raise CdcxError(5, f"cdcx_create failed (device {device})")

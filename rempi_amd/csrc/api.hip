@@ -76,6 +76,7 @@ constexpr const char* kAliasWnf = "chain";    // with_next flags       <- chain 
 struct cdcx_ctx {
   int device = 0;
   int gzip = 0;  // REMPI_GZIP: host-buffer encode/decode apply the zlib stage (gzip_stage.hip)
+  bool rep = false;  // REMPI_ENCODE=7: epoch lines only (rempi_encoder_rep.cpp:50-146)
   int64_t max_len = 131072;
   std::string err;
   std::map<std::string, DevBuf> bufs;
@@ -426,6 +427,9 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   if (std::any_of(units.begin(), units.end(), [](const Unit& u) { return u.S == -1; }))  // > 256 sources
     c->launch(K_EPOCH, k_epoch<2 * kMaxUnitSources>, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank,
               d_ep_clk, d_err);
+  int32_t* d_pid = nullptr;
+  int32_t* d_pdl = nullptr;
+  if (!c->rep) {  // the rep encoder writes no matched-event sections: no chain, no edit sequence
   Seg* d_segs = c->buf<Seg>("segs", nsegs);
   c->launch(K_SEG_LIST, k_seg_list, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_segend, d_segs);
   int32_t* d_seghist = c->buf<int32_t>("seghist", 4096);
@@ -492,12 +496,13 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
             (const uint8_t*)d_chain, d_posA, d_crow, d_seq);
   c->launch(K_POSITIONS, k_pos_cols, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_inv,
             (const uint8_t*)d_chain, (const int32_t*)d_posA, (const int32_t*)d_crow, d_seq, d_sx);
-  int32_t* d_pid = c->buf<int32_t>("pid", N);
-  int32_t* d_pdl = c->buf<int32_t>("pdl", N);
+  d_pid = c->buf<int32_t>("pid", N);
+  d_pdl = c->buf<int32_t>("pdl", N);
   c->launch(K_DELTAS, k_deltas, dim3(NU), dim3(256), s, (const Unit*)d_units, (const uint32_t*)d_seq, (const int32_t*)d_sx,
             d_pid, d_pdl);
   c->check_err(d_err, s);
   units = c->download(d_units, NU, s);
+  }
 
   // Sizes, footer scratch, offsets.
   std::vector<int64_t> fk_off(R + 1, 0), fb_off(R + 1, 0);
@@ -544,7 +549,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
       for (int32_t k = 0; k < ch.n_units; k++, ui++) {
         Unit& u = units[ui];
         u.out_off = q;
-        q += 72 + 16ll * u.S + 8ll * u.W + 8ll * u.M + 16ll * u.U + 8ll * u.P;
+        q += 72 + 16ll * u.S + (c->rep ? 0 : 8ll * u.W + 8ll * u.M + 16ll * u.U + 8ll * u.P);
       }
       ch.payload = q - pos - 8;
       pos = q;
@@ -561,7 +566,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int2* d_keys = c->buf<int2>("keys", key_run);
   c->launch(K_WRITE_UNITS, k_write_units, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_midx,
             (const int32_t*)d_wp, (const int32_t*)d_run_id, (const uint64_t*)d_run_cnt, (const uint64_t*)d_ep_rank,
-            (const uint64_t*)d_ep_clk, (const int32_t*)d_pid, (const int32_t*)d_pdl, d_out);
+            (const uint64_t*)d_ep_clk, (const int32_t*)d_pid, (const int32_t*)d_pdl, (int32_t)c->rep, d_out);
   c->launch(K_CHUNK_HEADERS, k_chunk_headers, dim3(blocks(C, 256)), dim3(256), s, (const Chunk*)d_chunks, C, d_out);
   c->launch(K_FOOTER_WRITE, k_footer_write, dim3(blocks(R, 64)), dim3(64), s, (const int64_t*)d_fk_off,
             (const int64_t*)d_fb_off, (const uint64_t*)d_fkey, (const int32_t*)d_fnext, (const int32_t*)d_fbucket,
@@ -766,6 +771,11 @@ cdcx_ctx* cdcx_create(const cdcx_opts* opts) {
       return nullptr;
     }
     c->gzip = opts->gzip;
+    if (opts->encode != 0 && opts->encode != 4 && opts->encode != 7) {
+      delete c;
+      return nullptr;
+    }
+    c->rep = opts->encode == 7;
   }
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || c->device < 0 || c->device >= n || hipSetDevice(c->device) != hipSuccess) {

@@ -1033,14 +1033,19 @@ __global__ void __launch_bounds__(256) k_write_units(const Unit* __restrict__ un
                                                      const uint64_t* __restrict__ run_cnt,
                                                      const uint64_t* __restrict__ ep_rank,
                                                      const uint64_t* __restrict__ ep_clk, const int32_t* __restrict__ pid,
-                                                     const int32_t* __restrict__ pdl, uint8_t* __restrict__ out) {
-  const Unit u = units[blockIdx.x];
+                                                     const int32_t* __restrict__ pdl, int32_t rep,
+                                                     uint8_t* __restrict__ out) {
+  Unit u = units[blockIdx.x];
   const int64_t a = u.a;
   uint8_t* o = out + u.out_off;
   const int t = threadIdx.x;
+  // REMPI_ENCODE=7 (rempi_encoder_rep.cpp:50-146): the same table with every section after
+  // the epoch line empty (lengths and sizes 0); the count stays the matched-event count.
+  const int32_t count = u.M;
+  if (rep) u.W = u.M = u.U = u.P = 0;
   if (t == 0) {
     st_u32(o, (uint32_t)u.set_id);
-    st_u32(o + 4, (uint32_t)u.M);
+    st_u32(o + 4, (uint32_t)count);
     st_u64(o + 8, 8ull * u.S);
   }
   uint8_t* p = o + 16;

@@ -55,3 +55,17 @@ def load_gzip(name):
     for k in ("rempi", "rempi_gz", "tables"):
         d[k] = d[k].tobytes()
     return d
+
+
+def rep_names():
+    """Fixtures of the rep encoder, REMPI_ENCODE=7 (tests/golden/make_rep_golden.py)."""
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "rep_*.npz")))
+
+
+def load_rep(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    d["max_len"] = int(d["max_len"])
+    for k in ("rempi_rep", "tables"):
+        d[k] = d[k].tobytes()
+    return d

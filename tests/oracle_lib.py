@@ -25,6 +25,8 @@ def lib():
         P = ctypes.POINTER
         u8p, i32p, i64p = P(ctypes.c_uint8), P(ctypes.c_int32), P(ctypes.c_int64)
         L.oracle_encode.argtypes = [i32p, ctypes.c_size_t, ctypes.c_int64, P(u8p), P(ctypes.c_size_t), P(ctypes.c_size_t)]
+        L.oracle_encode_ex.argtypes = [i32p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int, P(u8p), P(ctypes.c_size_t),
+                                       P(ctypes.c_size_t)]
         L.oracle_decode.argtypes = [u8p, ctypes.c_size_t, P(u8p), P(ctypes.c_size_t)]
         L.oracle_cdc_pairs.argtypes = [i32p, ctypes.c_int64, i32p, i32p, i64p]
         L.oracle_decode_perm.argtypes = [i64p, i64p, ctypes.c_int64, ctypes.c_int64, i32p]
@@ -49,14 +51,15 @@ class OracleError(RuntimeError):
         self.code = code
 
 
-def encode(recs: np.ndarray, max_len: int = 131072):
-    """-> (file bytes, footer offset)."""
+def encode(recs: np.ndarray, max_len: int = 131072, rep: bool = False):
+    """-> (file bytes, footer offset); rep: the REMPI_ENCODE=7 encoder (epoch lines only)."""
     L = lib()
     r = np.ascontiguousarray(recs, dtype=np.int32).reshape(-1, 8)
     out = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
     foff = ctypes.c_size_t()
-    rc = L.oracle_encode(_ptr(r, ctypes.c_int32), r.shape[0], max_len, ctypes.byref(out), ctypes.byref(n), ctypes.byref(foff))
+    rc = L.oracle_encode_ex(_ptr(r, ctypes.c_int32), r.shape[0], max_len, int(rep), ctypes.byref(out), ctypes.byref(n),
+                            ctypes.byref(foff))
     if rc:
         raise OracleError(rc)
     data = ctypes.string_at(out, n.value)
@@ -184,12 +187,14 @@ def have_ref() -> bool:
     return os.path.exists(REF_BIN)
 
 
-def ref_encode(recs: np.ndarray, max_len: int = 131072, gzip: bool = False):
-    """Run the reference encoder (oracle/_ref/ref_cdc) -> (bytes, seconds); gzip: REMPI_GZIP=1."""
+def ref_encode(recs: np.ndarray, max_len: int = 131072, gzip: bool = False, rep: bool = False):
+    """Run the reference encoder (oracle/_ref/ref_cdc) -> (bytes, seconds); gzip: REMPI_GZIP=1;
+    rep: the REMPI_ENCODE=7 encoder (rempi_encoder_rep, epoch lines only)."""
     with tempfile.TemporaryDirectory() as d:
         inp, outp = os.path.join(d, "in.rec"), os.path.join(d, "out.rempi")
         np.ascontiguousarray(recs, dtype=np.int32).tofile(inp)
-        res = subprocess.run([REF_BIN, "encode", inp, outp, str(max_len)] + (["gzip"] if gzip else []),
+        res = subprocess.run([REF_BIN, "encode", inp, outp, str(max_len)] + (["gzip"] if gzip else []) +
+                             (["rep"] if rep else []),
                              capture_output=True, text=True)
         if res.returncode != 0:
             raise RuntimeError(f"ref encode failed rc={res.returncode}: {res.stderr[-500:]}")
