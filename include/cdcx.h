@@ -160,6 +160,39 @@ int cdcx_decode_batch_device(cdcx_ctx* ctx, int32_t n_ranks, const uint8_t* d_in
                              const int32_t** d_perm, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Replay-side streaming decode (config 5).  Replaces one
+ * read_record_file (:933-978) + decode (:1016-1299) + cdc_prepare_decode_indices
+ * (:1301-1386) loop per rank process, which progress_decoding (:851-930) runs over
+ * REMPI_DIR/rank_<r>.rempi, by one pass over many rank files.
+ *
+ * The n_files files at paths[] are decoded in batches of consecutive files of about
+ * batch_bytes (<= 0: 256 MiB) each.  One host thread per context runs its own batches on its
+ * own non-blocking HIP stream: file reads into a pinned host buffer (inflated first on a
+ * gzip context), H2D, the decode kernels, D2H of the tables, so one context's reads and
+ * copies overlap another's kernels.  Contexts may share a device.  For every file, in
+ * completion order, sink(user, i, dump, n_words) receives file i's table dump (the int64
+ * format of cdcx_decode_stream, valid only during the call).  Sink calls are serialised.  A
+ * non-zero sink return stops the pipeline with CDCX_ERR_ARG.  stats (may be NULL) gets
+ * totals.  On error the failing context's cdcx_last_error says why. */
+typedef int (*cdcx_replay_sink)(void* user, int32_t file_index, const int64_t* dump, size_t n_words);
+typedef struct cdcx_replay_stats {
+  int64_t files;      /* rank files decoded */
+  int64_t file_bytes; /* bytes read from the files (before inflating) */
+  int64_t chunks;     /* chunks (read_record_file calls that returned data) */
+  int64_t units;      /* matching-set tables */
+  int64_t records;    /* canonical records the tables describe: matched + unmatched runs */
+  int64_t batches;    /* device batches */
+  int64_t dump_bytes; /* bytes of table dumps handed to the sink */
+  double seconds;     /* wall time of the whole call */
+  double read_s;      /* thread-seconds per phase, summed over contexts: file reads (+ inflate) */
+  double device_s;    /* H2D + decode kernels + D2H of the tables */
+  double dump_s;      /* host formatting of the per-rank table dumps */
+  double sink_s;      /* inside the sink */
+} cdcx_replay_stats;
+int cdcx_replay_decode_files(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths,
+                             int64_t batch_bytes, cdcx_replay_sink sink, void* user, cdcx_replay_stats* stats);
+
+/* ---------------------------------------------------------------------------------------
  * Synthetic workload (definition in DESIGN.md "Synthetic traces"), generated
  * directly in device memory: n_ranks consecutive ranks starting at first_rank of a job of
  * world_size ranks, ~events_per_rank records each.  *d_rec (context-owned) and rec_off

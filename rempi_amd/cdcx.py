@@ -46,6 +46,16 @@ class GenParams(ctypes.Structure):
 P = ctypes.POINTER
 _u8p, _i32p, _i64p, _vp = P(ctypes.c_uint8), P(ctypes.c_int32), P(ctypes.c_int64), ctypes.c_void_p
 
+
+class ReplayStats(ctypes.Structure):
+    _fields_ = [("files", ctypes.c_int64), ("file_bytes", ctypes.c_int64), ("chunks", ctypes.c_int64),
+                ("units", ctypes.c_int64), ("records", ctypes.c_int64), ("batches", ctypes.c_int64),
+                ("dump_bytes", ctypes.c_int64), ("seconds", ctypes.c_double), ("read_s", ctypes.c_double),
+                ("device_s", ctypes.c_double), ("dump_s", ctypes.c_double), ("sink_s", ctypes.c_double)]
+
+
+_REPLAY_SINK = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.c_int32, _i64p, ctypes.c_size_t)
+
 _SIGNATURES = {
     "cdcx_create": ([P(_Opts)], _vp),
     "cdcx_destroy": ([_vp], None),
@@ -63,6 +73,8 @@ _SIGNATURES = {
     "cdcx_decode_stream": ([_vp, _u8p, ctypes.c_size_t, P(_u8p), P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_reconstruct_stream": ([_vp, _u8p, ctypes.c_size_t, _i32p, ctypes.c_size_t, P(_i32p), P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_decode_batch_device": ([_vp, ctypes.c_int32, _vp, _i64p, _i64p, _vp, ctypes.c_int64, P(_vp), _i64p, P(_vp), _vp], ctypes.c_int),
+    "cdcx_replay_decode_files": ([P(_vp), ctypes.c_int32, ctypes.c_int32, P(ctypes.c_char_p), ctypes.c_int64,
+                                  _REPLAY_SINK, _vp, P(ReplayStats)], ctypes.c_int),
     "cdcx_generate_device": ([_vp, P(GenParams), ctypes.c_int32, ctypes.c_int32, P(_vp), _i64p, _vp], ctypes.c_int),
     "cdcx_generate_host": ([P(GenParams), ctypes.c_int32, P(_i32p), P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_set_profiling": ([_vp, ctypes.c_int], ctypes.c_int),
@@ -369,6 +381,38 @@ def memcpy_async(dst: int, src: int, nbytes: int, kind: int, stream: int) -> Non
         rc = hip().hipMemcpyAsync(dst, src, nbytes, kind, stream)
         if rc:
             raise CdcxError(5, f"hipMemcpyAsync failed ({rc})")
+
+
+def replay_decode_files(contexts, paths, sink=None, batch_bytes: int = 0) -> dict:
+    """Streaming replay decode of many rank files (cdcx_replay_decode_files): one host
+    thread and HIP stream per context.  sink(file_index, dump_bytes) receives each file's
+    table dump (the bytes cdcx_decode_stream returns) in completion order; a sink that
+    raises or returns a true value stops the pipeline.  -> the call's totals."""
+    L = lib()
+    ctxs = (_vp * len(contexts))(*[c._c for c in contexts])
+    enc = [os.fsencode(p) for p in paths]
+    arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+    failure = []
+
+    def _sink(_user, i, dump, n):
+        if sink is None:
+            return 0
+        try:
+            data = ctypes.string_at(dump, 8 * n) if n else b""
+            return 1 if sink(int(i), data) else 0
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            failure.append(e)
+            return 1
+
+    cb = _REPLAY_SINK(_sink)
+    st = ReplayStats()
+    rc = L.cdcx_replay_decode_files(ctxs, len(contexts), len(enc), arr, int(batch_bytes), cb, None, ctypes.byref(st))
+    if failure:
+        raise failure[0]
+    if rc:
+        msgs = [L.cdcx_last_error(c._c).decode() for c in contexts]
+        raise CdcxError(rc, "replay_decode_files: " + "; ".join(m for m in msgs if m))
+    return {k: getattr(st, k) for k, _ in ReplayStats._fields_}
 
 
 class PinnedBuffer:

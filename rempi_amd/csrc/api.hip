@@ -5,13 +5,19 @@
 // device or a launch fails the call returns CDCX_ERR_HIP.
 #include <hip/hip_runtime.h>
 
+#include <sys/stat.h>
+
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/cdcx.h"
@@ -27,7 +33,7 @@ enum KernelId {
   K_SET_PRESENCE, K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_INC0, K_TILE_SUM, K_RANK_SCAN, K_TILE_P0,
   K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_WINDOW_RANK, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_G16, K_CHAIN_G64, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
   K_WRITE_UNITS, K_CHUNK_HEADERS, K_FOOTER_ORDER, K_FOOTER_WRITE, K_WRITE_KEYS,
-  K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS,
+  K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS, K_DEC_PACK,
   K_GEN_TILE_SUMS, K_GEN_RANK_SCAN, K_GEN_FRAMES, K_GEN_AKEYS, K_GEN_ARRIVAL, K_GEN_RECORDS,
   K_COUNT
 };
@@ -35,7 +41,7 @@ const char* kKernelNames[K_COUNT] = {
   "k_set_presence", "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_inc0", "k_tile_sum", "k_rank_scan",
   "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_window_rank", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
-  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records",
+  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records", "k_dec_pack_tables",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
 
 struct HipError {
@@ -90,6 +96,11 @@ struct cdcx_ctx {
   std::vector<Pending> pending;
   std::vector<hipEvent_t> event_pool;
   hipStream_t stream = nullptr;
+  struct Pinned {  // grow-only page-locked host buffer
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+  };
+  Pinned pin_in, pin_tab;  // replay pipeline: rank files in; packed decoded tables out
 
   // results of the last encode
   uint8_t* d_out = nullptr;
@@ -99,6 +110,7 @@ struct cdcx_ctx {
   std::vector<DUnit> dunits;
   std::vector<DChunk> dchunks;
   std::vector<int32_t> dfirst_unit, dnunits;
+  std::vector<int32_t> dcbase;  // first chunk of each rank file of the last decode (R + 1)
   int32_t* d_rec_out = nullptr;
   int64_t n_rec_out = 0;
   int32_t* d_perm = nullptr;
@@ -599,6 +611,8 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
     C += nch[r];
   }
   int32_t* d_cbase = c->upload("d_cbase", cbase, s);
+  c->dcbase = cbase;
+  c->dcbase.push_back(C);
   DChunk* d_ch = c->buf<DChunk>("d_chunks", C);
   c->launch(K_DEC_LIST_CHUNKS, k_dec_list_chunks, dim3(blocks(R, 64)), dim3(64), s, d_in, (const int64_t*)d_off,
             (const int32_t*)d_cbase, (const int32_t*)d_nch, R, d_ch);
@@ -696,54 +710,126 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
 
 // Host-side table dump of the last decode (tests / drop-in shim): mirrors the fields the
 // reference keeps in rempi_encoder_input_format_test_table after decode().
-std::vector<int64_t> tables_dump(cdcx_ctx* c, const uint8_t* in, hipStream_t s) {
-  const size_t NU = c->dunits.size();
-  int64_t wb = 0, ko = 0;
-  for (auto& u : c->dunits) { wb = std::max(wb, u.wbase + u.M + 1); ko = std::max(ko, u.key_off + u.M); }
-  std::vector<uint64_t> wpd = c->download(c->buf<uint64_t>(kAliasWpd, 0), wb, s);
-  std::vector<uint64_t> uidd = c->download(c->buf<uint64_t>(kAliasUidd, 0), wb, s);
-  std::vector<uint64_t> idd = c->download(c->buf<uint64_t>(kAliasIdd, 0), wb, s);
-  std::vector<uint64_t> dld = c->download(c->buf<uint64_t>(kAliasDld, 0), wb, s);
-  std::vector<int32_t> perm = c->download(c->d_perm, ko, s);
-  (void)NU;
-  std::vector<int64_t> d;
-  auto u64at = [&](int64_t o) {
-    uint64_t v;
-    memcpy(&v, in + o, 8);
-    return (int64_t)v;
-  };
-  for (size_t k = 0; k < c->dchunks.size(); k++) {
+uint8_t* pinned(cdcx_ctx::Pinned& b, size_t bytes) {
+  if (bytes > b.cap) {
+    if (b.p) HIPCHK(hipHostFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 20);
+    if (hipHostMalloc(reinterpret_cast<void**>(&b.p), want, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      b.p = nullptr;
+      throw CdcxError{CDCX_ERR_NOMEM, "pinned host allocation of " + std::to_string(want) + " bytes failed"};
+    }
+    b.cap = want;
+  }
+  return b.p;
+}
+
+// The decoded per-unit arrays of the last decode, packed on the device (k_dec_pack_tables:
+// per unit with_previous[W], unmatched ids[U], ids[P], delays[P]) and copied into pinned
+// host memory with perm[] in one D2H each.
+struct DecodedTables {
+  const uint64_t* pk = nullptr;  // packed words
+  std::vector<int64_t> pk_off;   // per unit, into pk
+  const int32_t* perm = nullptr;
+};
+
+DecodedTables download_tables(cdcx_ctx* c, hipStream_t s) {
+  const int32_t NU = (int32_t)c->dunits.size();
+  DecodedTables t;
+  t.pk_off.resize(NU + 1);
+  int64_t pw = 0, ko = 0;
+  for (int32_t q = 0; q < NU; q++) {
+    const DUnit& u = c->dunits[q];
+    t.pk_off[q] = pw;
+    pw += (int64_t)u.W + (u.Uc > 0 ? u.U : 0) + 2ll * u.P;
+    ko = std::max(ko, u.key_off + u.M);
+  }
+  t.pk_off[NU] = pw;
+  uint8_t* h = pinned(c->pin_tab, (size_t)(8 * pw + 4 * ko + 8));
+  if (NU) {
+    int64_t* d_pko = c->upload("d_pack_off", t.pk_off, s);
+    uint64_t* d_pk = c->buf<uint64_t>("d_pack", (size_t)pw);
+    c->launch(K_DEC_PACK, k_dec_pack_tables, dim3(NU), dim3(256), s, (const DUnit*)c->buf<DUnit>("d_units", 0),
+              (const int64_t*)d_pko, (const uint64_t*)c->buf<uint64_t>(kAliasWpd, 0),
+              (const uint64_t*)c->buf<uint64_t>(kAliasUidd, 0), (const uint64_t*)c->buf<uint64_t>(kAliasIdd, 0),
+              (const uint64_t*)c->buf<uint64_t>(kAliasDld, 0), d_pk);
+    if (pw) HIPCHK(hipMemcpyAsync(h, d_pk, 8 * pw, hipMemcpyDeviceToHost, s));
+    if (ko) HIPCHK(hipMemcpyAsync(h + 8 * pw, c->d_perm, 4 * ko, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  t.pk = reinterpret_cast<const uint64_t*>(h);
+  t.perm = reinterpret_cast<const int32_t*>(h + 8 * pw);
+  return t;
+}
+
+// Dump of chunks [k0, k1) of the last decode (one rank file's chunks when the batch held
+// several).  `in` is the host image of the decoded batch buffer (same offsets as d_in).
+void dump_chunks(const cdcx_ctx* c, const DecodedTables& t, const uint8_t* in, int32_t k0, int32_t k1,
+                 std::vector<int64_t>& d) {
+  std::vector<std::pair<uint64_t, int32_t>> um;  // (unmatched id, position): sorted, last write wins
+  for (int32_t k = k0; k < k1; k++) {
     std::map<int32_t, int32_t> bysid;  // test_tables_map: last table with an id wins
     for (int32_t q = 0; q < c->dnunits[k]; q++) bysid[c->dunits[c->dfirst_unit[k] + q].set_id] = c->dfirst_unit[k] + q;
     d.push_back((int64_t)bysid.size());
     for (auto& kv : bysid) {
       const DUnit& u = c->dunits[kv.second];
-      d.push_back(u.set_id);
-      d.push_back(u.M);
-      d.push_back(u.S);
-      for (int32_t i = 0; i < u.S; i++) d.push_back(u64at(u.ep_off + 8ll * i));
-      d.push_back(u.S);
-      for (int32_t i = 0; i < u.S; i++) d.push_back(u64at(u.ep_off + 8ll * (u.S + i)));
-      d.push_back(u.W);
-      for (int32_t i = 0; i < u.W; i++) d.push_back((int64_t)wpd[u.wbase + i]);
-      d.push_back(u.Mi);
-      for (int32_t i = 0; i < u.Mi; i++) d.push_back(u64at(u.mi_off + 8ll * i));
-      std::map<uint64_t, uint64_t> um;
-      if (u.Uc > 0)
-        for (int32_t i = 0; i < u.U; i++) um[uidd[u.wbase + i]] = (uint64_t)u64at(u.ucnt_off + 8ll * i);
-      d.push_back((int64_t)um.size());
-      for (auto& p : um) {
-        d.push_back((int64_t)p.first);
-        d.push_back((int64_t)p.second);
+      const uint64_t* wpd = t.pk + t.pk_off[kv.second];
+      const uint64_t* uidd = wpd + u.W;
+      const uint64_t* idd = uidd + (u.Uc > 0 ? u.U : 0);
+      const uint64_t* dld = idd + u.P;
+      um.clear();
+      if (u.Uc > 0) {
+        for (int32_t i = 0; i < u.U; i++) um.emplace_back(uidd[i], i);
+        std::stable_sort(um.begin(), um.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+        size_t w = 0;  // keep the last of equal ids (unordered_map operator[] assignment)
+        for (size_t i = 0; i < um.size(); i++) {
+          if (w && um[w - 1].first == um[i].first) w--;
+          um[w++] = um[i];
+        }
+        um.resize(w);
       }
-      d.push_back(u.P);
-      for (int32_t i = 0; i < u.P; i++) d.push_back((int64_t)idd[u.wbase + i]);
-      d.push_back(u.P);
-      for (int32_t i = 0; i < u.P; i++) d.push_back((int64_t)dld[u.wbase + i]);
-      d.push_back(u.M);
-      for (int32_t i = 0; i < u.M; i++) d.push_back(perm[u.key_off + i]);
+      const size_t n0 = d.size();
+      d.resize(n0 + 10 + 2 * (size_t)u.S + u.W + u.Mi + 2 * um.size() + 2 * (size_t)u.P + u.M);
+      int64_t* o = d.data() + n0;
+      *o++ = u.set_id;
+      *o++ = u.M;
+      *o++ = u.S;
+      memcpy(o, in + u.ep_off, 8ull * u.S);
+      o += u.S;
+      *o++ = u.S;
+      memcpy(o, in + u.ep_off + 8ll * u.S, 8ull * u.S);
+      o += u.S;
+      *o++ = u.W;
+      memcpy(o, wpd, 8ull * u.W);
+      o += u.W;
+      *o++ = u.Mi;
+      memcpy(o, in + u.mi_off, 8ull * u.Mi);
+      o += u.Mi;
+      *o++ = (int64_t)um.size();
+      for (auto& p : um) {
+        uint64_t cnt;
+        memcpy(&cnt, in + u.ucnt_off + 8ll * p.second, 8);
+        *o++ = (int64_t)p.first;
+        *o++ = (int64_t)cnt;
+      }
+      *o++ = u.P;
+      memcpy(o, idd, 8ull * u.P);
+      o += u.P;
+      *o++ = u.P;
+      memcpy(o, dld, 8ull * u.P);
+      o += u.P;
+      *o++ = u.M;
+      const int32_t* pm = t.perm + u.key_off;
+      for (int32_t i = 0; i < u.M; i++) o[i] = pm[i];
     }
   }
+}
+
+std::vector<int64_t> tables_dump(cdcx_ctx* c, const uint8_t* in, hipStream_t s) {
+  std::vector<int64_t> d;
+  dump_chunks(c, download_tables(c, s), in, 0, (int32_t)c->dchunks.size(), d);
   return d;
 }
 
@@ -791,6 +877,8 @@ void cdcx_destroy(cdcx_ctx* c) {
   (void)hipSetDevice(c->device);
   for (auto& kv : c->bufs)
     if (kv.second.p) (void)hipFree(kv.second.p);
+  if (c->pin_in.p) (void)hipHostFree(c->pin_in.p);
+  if (c->pin_tab.p) (void)hipHostFree(c->pin_tab.p);
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   for (auto& p : c->pending) {
     (void)hipEventDestroy(p.a);
@@ -1041,6 +1129,171 @@ int cdcx_decode_batch_device(cdcx_ctx* c, int32_t n_ranks, const uint8_t* d_in, 
     *n_rec_out = c->n_rec_out;
     *d_perm = c->d_perm;
   });
+}
+
+// Replay-side streaming decode: one host thread per context, each
+// taking whole batches of consecutive rank files off a shared counter.
+}  // extern "C"
+
+namespace {
+
+struct ReplayJob {
+  const char* const* paths;
+  std::vector<int64_t> size;                  // file sizes (stat)
+  std::vector<int32_t> first;                 // batch b = files [first[b], first[b + 1])
+  std::atomic<int32_t> next{0};
+  std::atomic<bool> stop{false};
+  std::mutex sink_mu;
+  cdcx_replay_sink sink;
+  void* user;
+  std::atomic<int64_t> chunks{0}, units{0}, records{0}, bytes{0}, dump_bytes{0};
+  std::atomic<int64_t> ns_read{0}, ns_device{0}, ns_dump{0}, ns_sink{0};  // thread time per phase
+};
+
+inline int64_t ns_since(std::chrono::steady_clock::time_point& t) {
+  const auto now = std::chrono::steady_clock::now();
+  const int64_t d = std::chrono::duration_cast<std::chrono::nanoseconds>(now - t).count();
+  t = now;
+  return d;
+}
+
+std::vector<uint8_t> read_file(const char* path, int64_t size) {
+  std::vector<uint8_t> v((size_t)size);
+  FILE* f = fopen(path, "rb");
+  if (!f) throw CdcxError{CDCX_ERR_ARG, std::string("cannot open ") + path};
+  const size_t got = size ? fread(v.data(), 1, (size_t)size, f) : 0;
+  fclose(f);
+  if (got != (size_t)size) throw CdcxError{CDCX_ERR_ARG, std::string("short read of ") + path};
+  return v;
+}
+
+void replay_batch(cdcx_ctx* c, ReplayJob& job, int32_t b, hipStream_t s) {
+  const int32_t f0 = job.first[b], f1 = job.first[b + 1], R = f1 - f0;
+  auto t = std::chrono::steady_clock::now();
+  std::vector<int64_t> off(R), len(R);
+  std::vector<std::vector<uint8_t>> plain;  // gzip contexts: inflated images
+  int64_t pos = 0;
+  if (c->gzip) {
+    plain.resize(R);
+    for (int32_t r = 0; r < R; r++) {
+      std::vector<uint8_t> z = read_file(job.paths[f0 + r], job.size[f0 + r]);
+      plain[r] = gunzip_file(z.data(), z.size());
+      off[r] = pos;
+      len[r] = (int64_t)plain[r].size();
+      pos = align_up(pos + len[r], 8);
+    }
+  } else {
+    for (int32_t r = 0; r < R; r++) {
+      off[r] = pos;
+      len[r] = job.size[f0 + r];
+      pos = align_up(pos + len[r], 8);
+    }
+  }
+  uint8_t* h = pinned(c->pin_in, (size_t)std::max<int64_t>(pos, 8));
+  for (int32_t r = 0; r < R; r++) {
+    if (c->gzip) {
+      if (len[r]) memcpy(h + off[r], plain[r].data(), (size_t)len[r]);
+      continue;
+    }
+    FILE* f = fopen(job.paths[f0 + r], "rb");
+    if (!f) throw CdcxError{CDCX_ERR_ARG, std::string("cannot open ") + job.paths[f0 + r]};
+    const size_t got = len[r] ? fread(h + off[r], 1, (size_t)len[r], f) : 0;
+    fclose(f);
+    if (got != (size_t)len[r]) throw CdcxError{CDCX_ERR_ARG, std::string("short read of ") + job.paths[f0 + r]};
+  }
+  job.ns_read += ns_since(t);
+  uint8_t* d = c->buf<uint8_t>("h_file", (size_t)std::max<int64_t>(pos, 8));
+  if (pos) HIPCHK(hipMemcpyAsync(d, h, (size_t)pos, hipMemcpyHostToDevice, s));
+  decode_batch(c, R, d, off, len, nullptr, 0, false, s);
+  const DecodedTables tb = download_tables(c, s);
+  job.ns_device += ns_since(t);
+  job.chunks += (int64_t)c->dchunks.size();
+  job.units += (int64_t)c->dunits.size();
+  job.records += c->n_rec_out;
+  std::vector<int64_t> dump;
+  for (int32_t r = 0; r < R; r++) {
+    dump.clear();
+    dump_chunks(c, tb, h, c->dcbase[r], c->dcbase[r + 1], dump);
+    job.dump_bytes += 8 * (int64_t)dump.size();
+    job.ns_dump += ns_since(t);
+    std::lock_guard<std::mutex> g(job.sink_mu);
+    if (job.stop) return;
+    if (job.sink(job.user, f0 + r, dump.data(), dump.size()) != 0)
+      throw CdcxError{CDCX_ERR_ARG, "replay sink stopped the pipeline at file " + std::to_string(f0 + r)};
+    job.ns_sink += ns_since(t);
+  }
+  for (int32_t r = 0; r < R; r++) job.bytes += job.size[f0 + r];
+}
+
+}  // namespace
+
+extern "C" {
+
+int cdcx_replay_decode_files(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths,
+                             int64_t batch_bytes, cdcx_replay_sink sink, void* user, cdcx_replay_stats* stats) {
+  if (!ctxs || n_ctx <= 0 || n_files < 0 || (n_files && !paths) || !sink) return CDCX_ERR_ARG;
+  for (int32_t i = 0; i < n_ctx; i++)
+    if (!ctxs[i]) return CDCX_ERR_ARG;
+  const auto t0 = std::chrono::steady_clock::now();
+  ReplayJob job;
+  job.paths = paths;
+  job.sink = sink;
+  job.user = user;
+  job.size.resize(n_files);
+  for (int32_t i = 0; i < n_files; i++) {
+    struct stat st;
+    if (!paths[i] || stat(paths[i], &st) != 0) {
+      ctxs[0]->err = std::string("cannot stat rank file ") + (paths[i] ? paths[i] : "(null)");
+      return CDCX_ERR_ARG;
+    }
+    job.size[i] = (int64_t)st.st_size;
+  }
+  const int64_t cap = batch_bytes > 0 ? batch_bytes : (int64_t)256 << 20;
+  job.first.push_back(0);
+  for (int32_t i = 0; i < n_files;) {
+    int64_t sum = 0;
+    int32_t j = i;
+    while (j < n_files && (j == i || sum + job.size[j] <= cap)) sum += job.size[j++];
+    job.first.push_back(j);
+    i = j;
+  }
+  const int32_t nb = (int32_t)job.first.size() - 1;
+  std::vector<int> rc(n_ctx, CDCX_OK);
+  auto worker = [&](int32_t w) {
+    cdcx_ctx* c = ctxs[w];
+    hipStream_t s = nullptr;
+    rc[w] = guarded(c, [&] {
+      HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+      for (int32_t b; !job.stop && (b = job.next++) < nb;) replay_batch(c, job, b, s);
+      HIPCHK(hipStreamSynchronize(s));
+    });
+    if (s) {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
+    if (rc[w] != CDCX_OK) job.stop = true;
+  };
+  std::vector<std::thread> th;
+  for (int32_t w = 1; w < n_ctx; w++) th.emplace_back(worker, w);
+  worker(0);
+  for (auto& t : th) t.join();
+  if (stats) {
+    stats->files = n_files;
+    stats->file_bytes = job.bytes;
+    stats->chunks = job.chunks;
+    stats->units = job.units;
+    stats->records = job.records;
+    stats->batches = nb;
+    stats->dump_bytes = job.dump_bytes;
+    stats->read_s = job.ns_read * 1e-9;
+    stats->device_s = job.ns_device * 1e-9;
+    stats->dump_s = job.ns_dump * 1e-9;
+    stats->sink_s = job.ns_sink * 1e-9;
+    stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  for (int32_t w = 0; w < n_ctx; w++)
+    if (rc[w] != CDCX_OK) return rc[w];
+  return CDCX_OK;
 }
 
 int cdcx_generate_host(const cdcx_gen_params* p, int32_t rank, int32_t** rec8, size_t* n_rec) {

@@ -688,3 +688,30 @@ __global__ void __launch_bounds__(256) k_dec_records(const DUnit* __restrict__ u
 }
 
 }  // namespace cdcx
+
+namespace cdcx {
+
+// Host copy of the decoded tables (replay pipeline / table dumps): one block per unit packs
+// the live prefixes of its M+1-strided scratch rows -- with_previous[W], unmatched ids[U],
+// pair ids[P], pair delays[P] -- contiguously at pk_off[unit], so the D2H carries only
+// what the tables hold.
+__global__ __launch_bounds__(256) void k_dec_pack_tables(const DUnit* __restrict__ units,
+                                                         const int64_t* __restrict__ pk_off,
+                                                         const uint64_t* __restrict__ wpd,
+                                                         const uint64_t* __restrict__ uidd,
+                                                         const uint64_t* __restrict__ idd,
+                                                         const uint64_t* __restrict__ dld,
+                                                         uint64_t* __restrict__ pk) {
+  const DUnit u = units[blockIdx.x];
+  uint64_t* o = pk + pk_off[blockIdx.x];
+  const int32_t U = u.Uc > 0 ? u.U : 0;
+  for (int32_t i = threadIdx.x; i < u.W; i += blockDim.x) o[i] = wpd[u.wbase + i];
+  o += u.W;
+  for (int32_t i = threadIdx.x; i < U; i += blockDim.x) o[i] = uidd[u.wbase + i];
+  o += U;
+  for (int32_t i = threadIdx.x; i < u.P; i += blockDim.x) o[i] = idd[u.wbase + i];
+  o += u.P;
+  for (int32_t i = threadIdx.x; i < u.P; i += blockDim.x) o[i] = dld[u.wbase + i];
+}
+
+}  // namespace cdcx

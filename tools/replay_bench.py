@@ -1,0 +1,92 @@
+"""Config 5 measurement: streaming replay decode of a REMPI_DIR.
+
+Writes R synthetic rank files (the bench workload at E events/rank, CDC-encoded on the GPU)
+into a directory, then decodes the whole directory with rempi_amd.replay (file read ->
+pinned host buffer -> H2D -> decode kernels -> D2H of the tables -> per-rank table dumps),
+and prints one JSON line.  Under torchrun each process takes the ranks r with
+r * WORLD_SIZE // R == RANK (contiguous blocks); no collective.
+
+    python tools/replay_bench.py --ranks 4096 --events 100000 --dir /tmp/rempi_dir
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from rempi_amd import cdcx, replay  # noqa: E402
+
+
+def write_dir(d, ranks, world, events, batch, device):
+    ctx = cdcx.Context(device=device)
+    s = cdcx.stream_create()
+    p = cdcx.default_gen_params(world_size=world, events_per_rank=events)
+    total = 0
+    try:
+        for b0 in range(ranks.start, ranks.stop, batch):
+            n = min(batch, ranks.stop - b0)
+            d_rec, rec_off = ctx.generate_device(p, b0, n, stream=s)
+            d_out, off, ln = ctx.encode_batch_device(d_rec, rec_off, stream=s)
+            cdcx.stream_sync(s)
+            img = cdcx.d2h(d_out, int(off[-1] + ln[-1]))
+            for i in range(n):
+                with open(os.path.join(d, f"rank_{b0 + i}.rempi"), "wb") as f:
+                    f.write(img[off[i]:off[i] + ln[i]].tobytes())
+            total += int(rec_off[-1])
+    finally:
+        ctx.close()
+    return total
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ranks", type=int, default=4096)
+    ap.add_argument("--events", type=int, default=100_000)
+    ap.add_argument("--dir", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "rempi_dir"))
+    ap.add_argument("--streams", type=int, default=4)
+    ap.add_argument("--batch-mb", type=int, default=256)
+    ap.add_argument("--gen-batch", type=int, default=64)
+    ap.add_argument("--repeat", type=int, default=2, help="decode passes (the first warms up)")
+    ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--py-sink", action="store_true", help="hand every dump to a Python sink (bytes copy)")
+    a = ap.parse_args()
+    ws, rank = int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("RANK", 0))
+    dev = int(os.environ.get("LOCAL_RANK", 0))
+    lo = next(r for r in range(a.ranks + 1) if r == a.ranks or r * ws // a.ranks == rank)
+    hi = next(r for r in range(lo, a.ranks + 1) if r == a.ranks or r * ws // a.ranks > rank)
+    d = f"{a.dir}_{rank}"
+    os.makedirs(d, exist_ok=True)
+    t0 = time.perf_counter()
+    records = write_dir(d, range(lo, hi), a.ranks, a.events, a.gen_batch, dev)
+    t_write = time.perf_counter() - t0
+    n_dumped = [0]
+
+    def sink(r, data):  # a consumer that takes each rank's tables (a bytes copy)
+        n_dumped[0] += 1
+
+    st = None
+    for _ in range(max(a.repeat, 1)):
+        n_dumped[0] = 0
+        st, _ = replay.decode_dir(d, a.streams, a.batch_mb << 20, 0, dev, sink if a.py_sink else None)
+    if not a.keep:
+        shutil.rmtree(d, ignore_errors=True)
+    out = {
+        "what": "config 5: streaming replay decode of REMPI_DIR rank files (read -> pinned -> H2D -> decode -> D2H "
+                "tables -> per-rank dumps), page cache warm",
+        "ranks": hi - lo, "world": a.ranks, "events_per_rank": a.events, "streams": a.streams,
+        "records_written": records, "write_s": round(t_write, 2),
+        "files": st["files"], "file_gb": round(st["file_bytes"] / 1e9, 3), "records_decoded": st["records"],
+        "chunks": st["chunks"], "units": st["units"], "batches": st["batches"], "seconds": round(st["seconds"], 3),
+        "record_gbps": round(32 * st["records"] / st["seconds"] / 1e9, 2),
+        "file_gbps": round(st["file_bytes"] / st["seconds"] / 1e9, 2),
+        "dump_gb": round(st["dump_bytes"] / 1e9, 3), "py_sink_dumps": n_dumped[0],
+        "thread_s": {k: round(st[k], 3) for k in ("read_s", "device_s", "dump_s", "sink_s")},
+    }
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
