@@ -124,6 +124,8 @@ struct cdcx_ctx {
   int dec_tier = getenv("CDCX_DEC_TIER") ? atoi(getenv("CDCX_DEC_TIER")) : 0;
   // 1: every unit takes the tile sort (skips the windowed rank), for tests
   int rank_tier = getenv("CDCX_RANK_TIER") ? atoi(getenv("CDCX_RANK_TIER")) : 0;
+  // blocks of the 16-lane chain tier (a work queue: fewer blocks leave CUs to other streams)
+  int64_t chain_grid = getenv("CDCX_CHAIN_GRID") ? std::max(1, atoi(getenv("CDCX_CHAIN_GRID"))) : 2048;
   int64_t chain_tier_counts[3] = {0, 0, 0};  // segments entering each tier in the last encode
 
   template <class T>
@@ -469,20 +471,27 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     const int32_t* nlist = d_cnt;
     int64_t n = nsegs;
     if (c->chain_tier <= 0) {
-      c->launch(K_CHAIN_G16, k_chain_grp<16>, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, blocks(n, 64)))),
-                dim3(256), s, (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par,
-                d_exta, d_topg, d_qn, d_ovf1, d_cnt + 1, d_err);
+      c->launch(K_CHAIN_G16, k_chain_grp<16>,
+                dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(c->chain_grid, blocks(n, 64)))), dim3(256), s,
+                (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par, d_exta,
+                d_topg, d_qn, d_ovf1, d_cnt + 1, d_err);
       list = d_ovf1;
       nlist = d_cnt + 1;
-      n = c->download(d_cnt + 1, 1, s)[0];
     }
-    c->chain_tier_counts[0] = nsegs;
-    c->chain_tier_counts[1] = n;
-    if (n > 0 && c->chain_tier <= 1) {
-      c->launch(K_CHAIN_G64, k_chain_grp<64>, dim3((unsigned)blocks(n, 4)), dim3(256), s, (const Unit*)d_units, d_segs, list,
-                nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par, d_exta, d_topg, d_qn, d_ovf2, d_cnt + 2, d_err);
+    // The 64-lane tier reads its segment count from the device (d_cnt + 1), so the host
+    // waits once, after it; only the rare lane tier needs the count on the host.
+    if (c->chain_tier <= 1) {
+      const int64_t g64 = c->chain_tier <= 0 ? std::min<int64_t>(1024, blocks(nsegs, 4)) : blocks(n, 4);
+      c->launch(K_CHAIN_G64, k_chain_grp<64>, dim3((unsigned)std::max<int64_t>(1, g64)), dim3(256), s,
+                (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par, d_exta,
+                d_topg, d_qn, d_ovf2, d_cnt + 2, d_err);
       list = d_ovf2;
-      n = c->download(d_cnt + 2, 1, s)[0];
+    }
+    {
+      const std::vector<int32_t> cnt = c->download(d_cnt, 3, s);
+      c->chain_tier_counts[0] = nsegs;
+      c->chain_tier_counts[1] = c->chain_tier <= 0 ? cnt[1] : nsegs;
+      if (c->chain_tier <= 1) n = cnt[2];
     }
     int2* d_leaves = n > 0 ? c->buf<int2>("leaves", w1n) : nullptr;  // lane tier only
     if (n > 0)
