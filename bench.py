@@ -1,29 +1,38 @@
 #!/usr/bin/env python3
 """CDC encode+decode throughput on MI355X (BASELINE.json metric).
 
-Workload (config 3 of BASELINE.json): synthetic traces of a 1024-rank job, 10M events per
-rank (gen.h / DESIGN.md "Synthetic traces").  Each GPU process holds one batch of
---ranks-per-gpu rank traces resident in HBM (they are generated on the device before the
-timed region; 1024 x 10M x 32 B = 328 GB does not fit one GPU at once).  One step = CDC
-encode of every rank of the batch (device bytes identical to the reference CPU encoder)
-+ CDC decode of the produced files back to tables and per-table event records.
-GPU g processes ranks [g*B, (g+1)*B) of the job: per-GPU work is fixed (weak scaling);
-the only collective is the final reduction of counters (RCCL all-reduce over xGMI).
+Workload (configs 3/4 of BASELINE.json): synthetic traces of a 1024-rank job, 10M events per
+rank (gen.h / DESIGN.md "Synthetic traces"): 327.7 GB of records, more than one GPU's HBM.
+The job's ranks are sharded over the GPUs in contiguous blocks (rank r -> GPU floor(r G / R),
+rempi_amd/shard.py); each GPU process walks its block in batches of at most --ranks-per-gpu
+rank traces resident in HBM.  Per batch: the traces are generated on the device (untimed),
+then W warmup and K timed steps run with inputs and outputs resident.  One step of a batch =
+CDC encode of every rank of the batch (device bytes identical to the reference CPU encoder)
++ CDC decode of the produced files back to tables and per-table event records; one step of
+the job = one step of every batch.  The timed regions of the batches are summed.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
-Prints one JSON line (rank 0).  value = 32 B x records encoded+decoded by all GPUs /
-max-over-ranks wall time of the K timed steps.
+Prints one JSON line (rank 0).  value = 32 B x records encoded+decoded by all GPUs in the K
+steps / max-over-ranks timed seconds.  The total work is the whole job whatever N is
+("strong" scaling); the only collective is the final reduction of counters (RCCL all-reduce).
+
+After the timed steps of a batch every rank is verified (outside the timed region): the
+decoded records of all ranks are compared on the device with the input they must reproduce,
+and the ranks pinned by tests/golden/config3_full.json (hashes of the reference encoder's
+file, the reference decoder's permutation and the expected records at full size) are hashed.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 import numpy as np
@@ -32,27 +41,33 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 RECORD_BYTES = 32
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+FIXTURE = os.path.join(ROOT, "tests", "golden", "config3_full.json")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--world", type=int, default=1024, help="ranks in the traced job")
     ap.add_argument("--events", type=int, default=10_000_000, help="events per rank trace")
-    ap.add_argument("--ranks-per-gpu", type=int, default=96, help="rank traces resident per GPU (one step)")
+    ap.add_argument("--ranks-per-gpu", type=int, default=96, help="rank traces resident per GPU (one batch)")
     ap.add_argument("--jitter", type=int, default=8)
     ap.add_argument("--max-len", type=int, default=131072, help="REMPI_MAX")
-    ap.add_argument("--verify-ranks", type=int, default=1, help="ranks checked byte-exact vs the CPU oracle")
+    ap.add_argument("--streams", type=int, default=4, help="lanes of a batch in flight per GPU (one HIP stream each)")
+    ap.add_argument("--max-batches", type=int, default=0,
+                    help="process only the first B batches of each GPU's block (0 = the whole block)")
+    ap.add_argument("--verify", type=int, default=1, help="verify every rank after the timed steps of its batch")
+    ap.add_argument("--oracle-ranks", type=int, default=1, help="ranks also encoded by the CPU oracle and compared")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the reference CPU CDC on a sample")
-    ap.add_argument("--cpu-sample-events", type=int, default=1_000_000)
-    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--cpu-sample-ranks", type=int, default=64, help="rank traces of the CPU sample (config 2: 64)")
+    ap.add_argument("--cpu-sample-events", type=int, default=1_000_000, help="events per rank of the CPU sample")
+    ap.add_argument("--cpu-workers", type=int, default=0, help="CPU worker processes (0 = the cores this process may use)")
     ap.add_argument("--kernel-report", action="store_true", help="print per-kernel times to stderr")
-    ap.add_argument("--streams", type=int, default=4, help="rank batches in flight per GPU (one HIP stream each)")
     ap.add_argument("--host-io", type=int, default=1, help="steps of the copy-inclusive measurement (0 = skip)")
-    return ap.parse_args()
+    ap.add_argument("--solo", type=int, default=2, help="steps of one lane alone for the roofline figure (0 = skip)")
+    return ap.parse_args(argv)
 
 
 def dist_env():
@@ -63,41 +78,82 @@ def dist_env():
 
 
 # ---------------------------------------------------------------------------------------
+def usable_cores() -> int:
+    """CPUs this process may run on (the GPU box grants a share of the host, which
+    os.cpu_count() does not show; OMP_NUM_THREADS carries it there)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        v = os.environ.get(var, "")
+        if v.isdigit() and int(v) > 0:
+            n = min(n, int(v))
+    return max(1, n)
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args):
-    """Reference CPU CDC (oracle/_ref/ref_cdc, compiled from the unmodified reference
-    sources) on a bounded sample of the same workload, one process per worker core."""
+    """Reference CPU CDC (oracle/_ref/ref_cdc, compiled from the unmodified reference sources;
+    the C++ restatement when that binary is absent) on config 2 of BASELINE.json -- 64 rank
+    traces x 1M events of the same generator -- one worker process per usable core, encode and
+    decode timed separately on the codec's own clock (trace loading and event construction
+    excluded, as the GPU figure excludes generation)."""
     import rempi_amd
 
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
 
-    workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
+    workers = args.cpu_workers or usable_cores()
+    n = args.cpu_sample_ranks
     p = rempi_amd.default_gen_params(world_size=args.world, jitter=args.jitter, events_per_rank=args.cpu_sample_events)
     kind = "reference" if O.have_ref() else "port"
     tmp = tempfile.mkdtemp(prefix="cdcx_cpu_")
-    recs_n = 0
-    files = []
-    for i in range(workers):
+    files, recs_n = [], 0
+    for i in range(n):
         r = rempi_amd.generate_host(p, i)
         recs_n += r.shape[0]
         f = os.path.join(tmp, f"rank_{i}.rec")
         r.tofile(f)
         files.append(f)
-    t0 = time.perf_counter()
-    if kind == "reference":
-        procs = [subprocess.Popen([O.REF_BIN, "encode", f, f + ".rempi", str(args.max_len)], stdout=subprocess.PIPE,
-                                  stderr=subprocess.DEVNULL) for f in files]
-        enc_s = [float(pr.communicate()[0].split()[1]) for pr in procs]
-        procs = [subprocess.Popen([O.REF_BIN, "decode", f + ".rempi", f + ".tables"], stdout=subprocess.PIPE,
-                                  stderr=subprocess.DEVNULL) for f in files]
-        dec_s = [float(pr.communicate()[0].split()[1]) for pr in procs]
-    else:
-        import multiprocessing as mp
+    enc_s, dec_s = [0.0] * n, [0.0] * n
+    busy = [0.0] * workers  # codec seconds per worker
+    nxt = [0]
+    lock = threading.Lock()
 
-        with mp.Pool(workers) as pool:
-            res = pool.map(_port_one, [(f, args.max_len) for f in files])
-        enc_s = [a for a, _ in res]
-        dec_s = [b for _, b in res]
+    def one(f):
+        if kind == "reference":
+            a = subprocess.run([O.REF_BIN, "encode", f, f + ".rempi", str(args.max_len)], capture_output=True, text=True)
+            b = subprocess.run([O.REF_BIN, "decode", f + ".rempi", f + ".tables"], capture_output=True, text=True)
+            return float(a.stdout.split()[1]), float(b.stdout.split()[1])
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--port-one", f, str(args.max_len)],
+                             capture_output=True, text=True)
+        e, d = out.stdout.split()[-2:]
+        return float(e), float(d)
+
+    def work(w):
+        while True:
+            with lock:
+                i = nxt[0]
+                nxt[0] += 1
+            if i >= n:
+                return
+            enc_s[i], dec_s[i] = one(files[i])
+            busy[w] += enc_s[i] + dec_s[i]
+
+    t0 = time.perf_counter()
+    ts = [threading.Thread(target=work, args=(w,)) for w in range(workers)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
     wall = time.perf_counter() - t0
     for f in files:
         for ext in ("", ".rempi", ".tables"):
@@ -105,17 +161,24 @@ def cpu_baseline(args):
                 os.remove(f + ext)
             except OSError:
                 pass
-    # Throughput on the codec's own clock (encode + decode per worker, workers in parallel)
-    per_worker = [e + d for e, d in zip(enc_s, dec_s)]
-    gbs = recs_n * RECORD_BYTES / max(per_worker) / 1e9
-    return {"value": round(gbs, 4), "unit": "GB/s", "cores": workers, "kind": kind,
-            "sample": f"{workers} rank traces x {args.cpu_sample_events} events of the same workload "
-                      f"(world {args.world}, J={args.jitter}), one process per core; encode "
-                      f"{np.mean(enc_s):.2f}s + decode {np.mean(dec_s):.2f}s per rank; wall {wall:.1f}s"}
+    try:
+        os.rmdir(tmp)
+    except OSError:
+        pass
+    nbytes = recs_n * RECORD_BYTES
+    return {"value": round(nbytes / max(busy) / 1e9, 4), "unit": "GB/s", "cores": workers, "kind": kind,
+            "encode_gbs": round(nbytes / (sum(enc_s) / workers) / 1e9, 4),
+            "decode_gbs": round(nbytes / (sum(dec_s) / workers) / 1e9, 4),
+            "encode_s_per_rank": round(float(np.mean(enc_s)), 3), "decode_s_per_rank": round(float(np.mean(dec_s)), 3),
+            "wall_s": round(wall, 2), "wall_gbs": round(nbytes / wall / 1e9, 4),
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "usable_cpus": usable_cores(),
+            "sample": f"config 2 in full: {n} rank traces x {args.cpu_sample_events} events of the same workload "
+                      f"(world {args.world}, J={args.jitter}), {workers} worker processes; value = bytes / "
+                      f"(encode + decode codec seconds of the busiest worker)"}
 
 
-def _port_one(a):
-    f, mx = a
+def port_one(f, mx):
+    """Child of cpu_baseline when the reference binary is absent: the C++ restatement."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
 
@@ -124,37 +187,40 @@ def _port_one(a):
     b, _ = O.encode(r, mx)
     t1 = time.perf_counter()
     O.decode(b)
-    return t1 - t0, time.perf_counter() - t1
+    print(t1 - t0, time.perf_counter() - t1)
 
 
 # ---------------------------------------------------------------------------------------
 class Lane:
-    """One rank batch on its own HIP stream and context (the bench runs --streams of them
-    side by side, one host thread each, so one batch's latency-bound phases overlap the
-    other's bandwidth-bound ones)."""
+    """One lane of a batch: a rank sub-batch on its own HIP stream and context (a batch runs
+    --streams of them side by side, one host thread each, so one lane's latency-bound phases
+    overlap another's bandwidth-bound ones)."""
 
-    def __init__(self, args, p, first, n, device):
+    def __init__(self, max_len, device):
         import rempi_amd
         from rempi_amd import cdcx
 
         self.cdcx = cdcx
-        self.first, self.n = first, n
         self.stream = cdcx.stream_create()
-        self.ctx = rempi_amd.Context(max_event_length=args.max_len, device=device)
-        self.d_rec, self.rec_off = self.ctx.generate_device(p, first, n, stream=self.stream)
-        cdcx.stream_sync(self.stream)
-        self.records = int(self.rec_off[-1])
+        self.ctx = rempi_amd.Context(max_event_length=max_len, device=device)
+        self.first = self.n = self.records = 0
         self.comp = 0
-        self.n_out = 0
+        self.last = None
+
+    def load(self, p, first, n):
+        """Generate ranks [first, first + n) of the job into this lane's device buffer."""
+        self.first, self.n = first, n
+        self.d_rec, self.rec_off = self.ctx.generate_device(p, first, n, stream=self.stream)
+        self.cdcx.stream_sync(self.stream)
+        self.records = int(self.rec_off[-1])
 
     def step(self):
         c = self.ctx
         d_out, off, ln = c.encode_batch_device(self.d_rec, self.rec_off, stream=self.stream)
         d_keys, n_keys = c.batch_sorted_keys()
-        _, n_out, _ = c.decode_batch_device(d_out, off, ln, d_keys, n_keys, stream=self.stream)
+        d_recs, n_out, d_perm = c.decode_batch_device(d_out, off, ln, d_keys, n_keys, stream=self.stream)
         self.comp += int(ln.sum())
-        self.n_out = n_out
-        return d_out, off, ln
+        self.last = (d_out, off, ln, d_recs, n_out, d_perm)
 
     def host_io_step(self, pin_rec, pin_files, pin_recs):
         """Copy-inclusive: records H2D from pinned host memory, encode + decode, rank files
@@ -168,10 +234,12 @@ class Lane:
         cd.memcpy_async(pin_recs.ptr, d_recs, n_out * RECORD_BYTES, 2, s)
         cd.stream_sync(s)
 
+    def close(self):
+        self.ctx.close()
+        self.cdcx.stream_destroy(self.stream)
+
 
 def run_lanes(lanes, fn, steps):
-    import threading
-
     errs = []
 
     def body(ln):
@@ -191,6 +259,69 @@ def run_lanes(lanes, fn, steps):
         raise errs[0]
 
 
+# ---------------------------------------------------------------------------------------
+def load_fixture(args):
+    """Reference hashes of full-size ranks, if they describe this run's workload."""
+    try:
+        fx = json.load(open(FIXTURE))
+    except (OSError, ValueError):
+        return {}
+    g = fx["generator"]
+    if (g["world_size"], g["events_per_rank"], g["jitter"], fx["max_len"]) != (args.world, args.events, args.jitter,
+                                                                               args.max_len):
+        return {}
+    return {int(k): v for k, v in fx["ranks"].items()}
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(memoryview(np.ascontiguousarray(a))).hexdigest()
+
+
+def verify_lane(ln: Lane, fixture: dict, oracle_ranks=(), p=None, max_len=131072) -> dict:
+    """Checks of the lane's last step (outside any timed region).
+    decode: every rank's decoded records against the input on the device (round trip), the
+            decoded record count, and -- for ranks the fixture pins -- SHA-256 of the records
+            and of the permutation against the reference decoder's.
+    encode: for fixture ranks, SHA-256 and length of the rank file against the reference
+            encoder's; for `oracle_ranks`, the bytes against the CPU restatement."""
+    cd = ln.cdcx
+    d_out, off, flen, d_recs, n_out, d_perm = ln.last
+    res = {"enc_ranks": 0, "enc_fail": 0, "dec_ranks": ln.n, "dec_fail": 0, "notes": []}
+    bad = ln.ctx.verify_roundtrip_device(ln.d_rec, stream=ln.stream)
+    if bad or n_out != ln.records:
+        res["dec_fail"] += ln.n
+        res["notes"].append(f"lane at rank {ln.first}: {bad} decoded records differ, {n_out} of {ln.records} records")
+    ro, po = ln.ctx.decode_rank_offsets(ln.n)
+    for q in range(ln.n):
+        r = ln.first + q
+        fx = fixture.get(r)
+        if fx is not None:
+            res["enc_ranks"] += 1
+            data = cd.d2h(d_out + int(off[q]), int(flen[q]))
+            if int(flen[q]) != fx["file_len"] or sha(data) != fx["file_sha256"]:
+                res["enc_fail"] += 1
+                res["notes"].append(f"rank {r}: file differs from the reference encoder's")
+            recs = cd.d2h(d_recs + int(ro[q]) * RECORD_BYTES, int(ro[q + 1] - ro[q]) * RECORD_BYTES)
+            perm = cd.d2h(d_perm + int(po[q]) * 4, int(po[q + 1] - po[q]) * 4)
+            if int(ro[q + 1] - ro[q]) != fx["records_out"] or sha(recs) != fx["records_sha256"] or \
+                    int(po[q + 1] - po[q]) != fx["matched"] or sha(perm) != fx["perm_sha256"]:
+                res["dec_fail"] += 1
+                res["notes"].append(f"rank {r}: decoded records / permutation differ from the reference's")
+        if r in oracle_ranks:
+            import rempi_amd
+
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import oracle_lib as O
+
+            want, _ = O.encode(rempi_amd.generate_host(p, r), max_len)
+            res["enc_ranks"] += 0 if fx is not None else 1
+            if cd.d2h(d_out + int(off[q]), int(flen[q])).tobytes() != want:
+                res["enc_fail"] += 1
+                res["notes"].append(f"rank {r}: file differs from the CPU restatement's")
+    return res
+
+
+# ---------------------------------------------------------------------------------------
 def main():
     args = parse()
     ws, rank, local = dist_env()
@@ -203,108 +334,137 @@ def main():
 
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import rempi_amd
-    from rempi_amd import cdcx
+    from rempi_amd import cdcx, shard
 
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib as O
-
-    from rempi_amd import shard
-
-    first, B = shard.shard(args.world, ws, rank, args.ranks_per_gpu)
+    shard.check_cover(args.world, ws)
+    first, count = shard.block(args.world, ws, rank)
+    plan = shard.batches(first, count, args.ranks_per_gpu)
+    if args.max_batches > 0:
+        plan = plan[:args.max_batches]
     p = rempi_amd.default_gen_params(world_size=args.world, jitter=args.jitter, events_per_rank=args.events)
-    sizes = shard.lane_sizes(B, args.streams)
-    S = len(sizes)
-    lanes, f = [], first
-    for n in sizes:
-        lanes.append(Lane(args, p, f, n, local))
-        f += n
-    n_records = sum(ln.records for ln in lanes)
+    fixture = load_fixture(args) if args.verify else {}
+    lanes = [Lane(args.max_len, local) for _ in range(max(1, min(args.streams, args.ranks_per_gpu)))]
 
-    run_lanes(lanes, Lane.step, args.warmup)
-    for ln in lanes:
-        ln.comp = 0
-        ln.ctx.set_profiling(True)
-        ln.ctx.reset_kernel_times()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    run_lanes(lanes, Lane.step, args.steps)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    free_b, total_b = torch.cuda.mem_get_info()
+    elapsed = 0.0
+    n_records = comp_bytes = 0
+    ver = {"enc_ranks": 0, "enc_fail": 0, "dec_ranks": 0, "dec_fail": 0, "notes": []}
     ktimes = {}
+    per_launch_records = 0
+    oracle_left = args.oracle_ranks if (args.verify and rank == 0) else 0
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t_job = time.perf_counter()
+    active = lanes
+    for (b_first, b_n) in plan:
+        sizes = shard.lane_sizes(b_n, len(lanes))
+        active = lanes[:len(sizes)]
+        at = b_first
+        for ln, n in zip(active, sizes):
+            ln.load(p, at, n)
+            at += n
+        run_lanes(active, Lane.step, args.warmup)
+        for ln in active:
+            ln.comp = 0
+            ln.ctx.set_profiling(True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run_lanes(active, Lane.step, args.steps)
+        torch.cuda.synchronize()
+        elapsed += time.perf_counter() - t0
+        for ln in active:
+            ln.ctx.set_profiling(False)
+            n_records += ln.records
+            comp_bytes += ln.comp
+        per_launch_records = max(per_launch_records, max(ln.records for ln in active))
+        if args.verify:
+            for ln in active:
+                take = list(range(ln.first, ln.first + min(oracle_left, ln.n)))
+                oracle_left -= len(take)
+                v = verify_lane(ln, fixture, take, p, args.max_len)
+                for k in ("enc_ranks", "enc_fail", "dec_ranks", "dec_fail"):
+                    ver[k] += v[k]
+                ver["notes"] += v["notes"]
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    job_wall = time.perf_counter() - t_job
+    free_b, total_b = torch.cuda.mem_get_info()
     for ln in lanes:
-        ln.ctx.set_profiling(False)
         for k, (ms, nl) in ln.ctx.kernel_times().items():
             a0, b0 = ktimes.get(k, (0.0, 0))
             ktimes[k] = (a0 + ms, b0 + nl)
-    comp_bytes = sum(ln.comp for ln in lanes)
+        ln.ctx.reset_kernel_times()
 
-    # Verification outside the timed region: byte-exact vs the CPU oracle for a sample of
-    # ranks; decoded record count bounded by the input.
-    fails = 0
-    checked = 0
-    for ln in lanes:
-        d_out, off, ln_ = ln.step()
-        for r in range(ln.n):
-            if checked >= args.verify_ranks:
-                break
-            host = rempi_amd.generate_host(p, ln.first + r)
-            want, _ = O.encode(host, args.max_len)
-            got = cdcx.d2h(d_out + int(off[r]), int(ln_[r])).tobytes()
-            fails += int(got != want)
-            checked += 1
-        fails += int(ln.n_out > ln.records)
+    # Dominant kernel alone on the GPU (one lane, nothing else in flight): its launch duration
+    # for the roofline figure.  Under --streams lanes the HIP events of a launch also cover the
+    # time the lane shares the CUs with the other lanes.
+    solo = {}
+    if args.solo and rank == 0 and active:
+        ln = active[0]
+        ln.ctx.set_profiling(True)
+        run_lanes([ln], Lane.step, args.solo)
+        ln.ctx.set_profiling(False)
+        solo = {k: v for k, v in ln.ctx.kernel_times().items() if v[1] > 0}
+        solo_records = ln.records
 
     # Copy-inclusive rate (host memory in and out); never `value`.
     host_io = None
-    if args.host_io and rank == 0:
+    if args.host_io and rank == 0 and active:
         pins = []
-        for ln in lanes:
+        for ln in active:
             pr = cdcx.PinnedBuffer(ln.records * RECORD_BYTES)
             cdcx.memcpy_async(pr.ptr, ln.d_rec, ln.records * RECORD_BYTES, 2, ln.stream)
             cdcx.stream_sync(ln.stream)
             pins.append((pr, cdcx.PinnedBuffer(ln.records * 24 + (1 << 20)), cdcx.PinnedBuffer(ln.records * RECORD_BYTES)))
-        run_lanes(lanes, lambda ln: ln.host_io_step(*pins[lanes.index(ln)]), 1)
+        run_lanes(active, lambda ln: ln.host_io_step(*pins[active.index(ln)]), 1)
         t1 = time.perf_counter()
-        run_lanes(lanes, lambda ln: ln.host_io_step(*pins[lanes.index(ln)]), args.host_io)
+        run_lanes(active, lambda ln: ln.host_io_step(*pins[active.index(ln)]), args.host_io)
         hio = time.perf_counter() - t1
-        host_io = {"value": round(n_records * RECORD_BYTES * args.host_io / hio / 1e9, 3), "unit": "GB/s",
-                   "steps": args.host_io,
+        nb = sum(ln.records for ln in active) * RECORD_BYTES * args.host_io
+        host_io = {"value": round(nb / hio / 1e9, 3), "unit": "GB/s", "steps": args.host_io,
                    "what": "H2D records from pinned host memory + encode + decode + D2H rank files and decoded records"}
         for pr in pins:
             for b in pr:
                 b.close()
 
-    counters, tmax = shard.reduce_counters([n_records * args.steps, comp_bytes, fails], elapsed, dist, "cuda")
-
+    counters, tmax = shard.reduce_counters(
+        [n_records * args.steps, comp_bytes, ver["enc_ranks"], ver["enc_fail"], ver["dec_ranks"], ver["dec_fail"],
+         count if args.max_batches <= 0 else sum(n for _, n in plan)], elapsed, dist, "cuda")
     total_records = counters[0]
     value = total_records * RECORD_BYTES / tmax / 1e9
-    comp_per_event = counters[1] / total_records
+    comp_per_event = counters[1] / max(total_records, 1)
 
-    # Roofline of the dominant kernel: algorithmic bytes per launch / mean launch time.
+    # Roofline of the dominant kernel: algorithmic bytes per launch / mean launch duration.
     kern = {k: v for k, v in ktimes.items() if v[1] > 0}
     dom = max(kern, key=lambda k: kern[k][0])
     dom_ms, dom_launches = kern[dom]
-    per_launch_records = n_records / S
-    algo = algorithmic_bytes(dom, per_launch_records, comp_per_event)
-    achieved = algo / (dom_ms / dom_launches / 1e3) / 1e9 if dom_launches else 0.0
+    if dom in solo:
+        s_ms, s_n = solo[dom]
+        launch_ms, launch_records = s_ms / s_n, solo_records
+    else:
+        launch_ms, launch_records = dom_ms / dom_launches, per_launch_records
+    algo = algorithmic_bytes(dom, launch_records, comp_per_event)
+    achieved = algo / (launch_ms / 1e3) / 1e9
 
     if args.kernel_report and rank == 0:
         tot = sum(v[0] for v in kern.values())
         for k, (ms, n) in sorted(kern.items(), key=lambda kv: -kv[1][0]):
-            print(f"  {k:22s} {ms / max(n, 1):10.3f} ms/launch x{n:4d}  {100 * ms / tot:5.1f}%", file=sys.stderr)
-        print(f"  timed {elapsed:.3f}s for {args.steps} steps on {S} streams; kernels sum {tot / 1e3:.3f}s",
-              file=sys.stderr)
+            so = solo.get(k)
+            print(f"  {k:22s} {ms / max(n, 1):10.3f} ms/launch x{n:5d}  {100 * ms / tot:5.1f}%"
+                  + (f"   alone {so[0] / so[1]:8.3f} ms" if so else ""), file=sys.stderr)
+        print(f"  timed {elapsed:.3f}s for {args.steps} steps x {len(plan)} batches on {len(lanes)} streams; "
+              f"kernels sum {tot / 1e3:.3f}s; job wall {job_wall:.1f}s", file=sys.stderr)
+        for note in ver["notes"][:20]:
+            print("  verify:", note, file=sys.stderr)
 
     cpu = None
     if args.cpu_baseline and rank == 0 and ws == 1:
         cpu = cpu_baseline(args)
 
     if rank == 0:
+        ranks_done = int(counters[6])
+        traffic = pmc_traffic()
         out = {
             "metric": "CDC encode+decode GB/s device-resident, 1024 ranks x 10M events; bit-exact",
             "value": round(value, 3),
@@ -314,31 +474,45 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(tmax / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic",
-            "config": {"workload": f"config3: {args.world}-rank job, {args.events} events/rank traces, "
-                                   f"{B} rank traces resident per GPU per step, encode+decode round trip",
-                       "ranks_per_gpu": B, "events_per_rank": args.events, "records_per_step_per_gpu": n_records,
-                       "jitter": args.jitter, "rempi_max": args.max_len, "streams_per_gpu": S,
+            "config": {"workload": f"config3/4: {args.world}-rank job x {args.events} events/rank, {ranks_done} rank traces "
+                                   f"processed per step over {ws} GPU(s) in batches of <= {args.ranks_per_gpu} resident "
+                                   f"traces, encode+decode round trip",
+                       "job_ranks": args.world, "ranks_processed": ranks_done, "batches_per_gpu": len(plan),
+                       "ranks_per_batch": args.ranks_per_gpu, "events_per_rank": args.events,
+                       "records_per_step": int(total_records / args.steps),
+                       "jitter": args.jitter, "rempi_max": args.max_len, "streams_per_gpu": len(lanes),
                        "compressed_bytes_per_event": round(comp_per_event, 3),
                        "hbm_used_gb": round((total_b - free_b) / 1e9, 1), "hbm_total_gb": round(total_b / 1e9, 1),
-                       "parallelism": f"dp{ws} (independent rank traces per GPU)",
-                       "verify_failures": int(counters[2])},
+                       "parallelism": f"dp{ws}: rank r -> GPU floor(r*{ws}/{args.world}), independent rank traces",
+                       "verify": {"encode_ranks": int(counters[2]), "encode_failures": int(counters[3]),
+                                  "decode_ranks": int(counters[4]), "decode_failures": int(counters[5]),
+                                  "how": "decode: device-side round trip of every rank + reference SHA-256 of records/"
+                                         "permutation for fixture ranks; encode: reference SHA-256 of the rank file "
+                                         "for fixture ranks (+ CPU restatement bytes for --oracle-ranks)"},
+                       "verify_failures": int(counters[3] + counters[5])},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": pmc_traffic(dom, per_launch_records), "traffic_source": PMC_TRAFFIC,
-                         "launch_ms": round(dom_ms / dom_launches, 3),
+                         "traffic": None if traffic is None or dom not in traffic["kernels"] else
+                         round(traffic["kernels"][dom]["bytes_per_record"] * launch_records),
+                         "traffic_source": PMC_TRAFFIC if traffic else None,
+                         "launch_ms": round(launch_ms, 3),
+                         "launch_ms_how": "HIP events, one lane alone on the GPU" if dom in solo else
+                                          "HIP events with all lanes in flight",
+                         "launch_ms_concurrent": round(dom_ms / dom_launches, 3),
                          "algorithmic_bytes_per_launch": round(algo),
-                         "pipeline_achieved": round(pipeline_bytes(comp_per_event) * total_records / tmax / 1e9, 2)},
+                         "pipeline_achieved": round(pipeline_bytes(comp_per_event) * total_records / tmax / 1e9, 2),
+                         "pipeline_algorithmic_bytes_per_record": round(pipeline_bytes(comp_per_event), 2),
+                         "pipeline_traffic_per_record": None if traffic is None else traffic.get("pipeline_bytes_per_record")},
             "cpu_baseline": cpu,
             "host_io": host_io,
         }
         print(json.dumps(out))
     for ln in lanes:
-        ln.ctx.close()
-        cdcx.stream_destroy(ln.stream)
+        ln.close()
     if dist:
         dist.destroy_process_group()
 
@@ -373,26 +547,30 @@ def algorithmic_bytes(kernel, n_records, c):
     return per * n_records
 
 
-PMC_TRAFFIC = "profiles/r01/pmc_traffic.json"
+PMC_TRAFFIC = "profiles/r02/pmc_traffic.json"
 
 
-def pmc_traffic(kernel, n_records):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-    (tools/pmc_traffic.py: read bytes = 2 x FETCH_SIZE per the gfx950 correction, checked on
-    k_tile_hist), scaled to the records one launch processes; None if not collected."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), PMC_TRAFFIC)
-    try:
-        k = json.load(open(path))["kernels"].get(kernel)
-    except (OSError, ValueError, KeyError):
-        return None
-    return None if k is None else round(k["bytes_per_record"] * n_records)
+def pmc_traffic():
+    """HBM bytes per record of every kernel from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes (tools/pmc_traffic.py); None if not collected."""
+    for rel in (PMC_TRAFFIC, "profiles/r01/pmc_traffic.json"):
+        try:
+            d = json.load(open(os.path.join(ROOT, rel)))
+            d.setdefault("kernels", {})
+            return d
+        except (OSError, ValueError):
+            continue
+    return None
 
 
 def pipeline_bytes(c):
-    """encode reads 32 B/event and writes c; decode reads c + 8m of sorted keys
-    and writes 32 B/event."""
+    """Algorithmic bytes of the whole path per record: encode reads 32 B/event and writes c;
+    decode reads c + 8m of sorted keys and writes 32 B/event."""
     return 64 + 2 * c + 8 * M_FRAC
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) == 4 and sys.argv[1] == "--port-one":
+        port_one(sys.argv[2], int(sys.argv[3]))
+    else:
+        main()

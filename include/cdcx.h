@@ -144,6 +144,57 @@ int cdcx_reconstruct_stream(cdcx_ctx* ctx, const uint8_t* in, size_t len,
                             const int32_t* sorted_keys, size_t n_keys, int32_t** rec8,
                             size_t* n_out);
 
+/* One decoded matching-set table of a chunk: the fields decode() (:1016-1299) leaves in
+ * rempi_encoder_input_format_test_table, as flat arrays.  Every pointer points into the one
+ * block that cdcx_tables.tables heads. */
+typedef struct cdcx_table {
+  int32_t set_id;                 /* test_tables_map key (matching_set_id) */
+  int32_t count;                  /* test_table->count: matched events */
+  size_t n_epoch;                 /* epoch_rank_vec / epoch_clock_vec, file order */
+  const uint64_t* epoch_rank;
+  const uint64_t* epoch_clock;
+  size_t n_with_previous;         /* with_previous_vec (inverse LP applied) */
+  const uint64_t* with_previous;
+  size_t n_matched_index;         /* matched_index_vec */
+  const uint64_t* matched_index;
+  size_t n_unmatched;             /* (id, count) in file order: unmatched_events_umap[id] = count */
+  const uint64_t* unmatched_id;
+  const uint64_t* unmatched_count;
+  size_t n_pairs;                 /* matched_events_id_vec / matched_events_delay_vec */
+  const uint64_t* ids;
+  const uint64_t* delays;
+  const int32_t* perm;            /* matched_events_permutated_indices_vec [count] */
+} cdcx_table;
+
+typedef struct cdcx_tables {
+  size_t n_tables;    /* tables of the chunk, ascending set id (std::map order); a later table
+                         with the same id replaces an earlier one, as test_tables_map[id] = does */
+  cdcx_table* tables; /* release with cdcx_free(tables): one block holds everything */
+} cdcx_tables;
+
+/* Host buffers: decode ONE chunk -- the payload read_record_file (:933-978) hands to decode()
+ * (:1016-1299; on a gzip context the zlib stream as stored in the file) -- into flat tables,
+ * including cdc_prepare_decode_indices (:1301-1386).  This is what a replacement of
+ * rempi_encoder_cdc::decode calls from progress_decoding's DECODE state (:877-882).
+ * CDCX_ERR_CORRUPT where the reference reports "Inconsistent size" (:1288) or would read out
+ * of bounds. */
+int cdcx_decode_chunk(cdcx_ctx* ctx, const uint8_t* payload, size_t len, cdcx_tables* out);
+
+/* Host buffers: records reconstruction of ONE chunk payload (decoded-record definition ii,
+ * the consumer side being cdc_decode_ordering :1655-1879): sorted_keys are the clock-sorted
+ * {source, clock} pairs of the chunk's tables in ascending set id.  *rec8 (cdcx_free) gets
+ * n_out x 8 int32. */
+int cdcx_reconstruct_chunk(cdcx_ctx* ctx, const uint8_t* payload, size_t len, const int32_t* sorted_keys,
+                           size_t n_keys, int32_t** rec8, size_t* n_out);
+
+/* The bytes write_footer (:2085-2126) appends at close_record_file: size_t 0 separator,
+ * size_t n, the n distinct ranks in the iteration order of the unordered_set<int>
+ * all_epoch_rank_uset after inserting epoch_ranks[0..n_in) in that order, then int32 0 (no
+ * matching-set-id map).  No context or GPU needed.  out may be NULL to query the size;
+ * otherwise *len holds its capacity on entry.  On return *len = footer bytes.
+ * CDCX_ERR_ARG when the capacity is too small. */
+int cdcx_footer(const int32_t* epoch_ranks, size_t n_in, uint8_t* out, size_t* len);
+
 /* Device-resident batch decode of n_ranks rank files (file r = in_len[r] bytes at
  * d_in + in_off[r], 8-byte aligned; host arrays) plus records reconstruction from d_keys
  * (int32 {source, clock} pairs, units in file order; NULL = tables only).  Outputs stay in
@@ -158,6 +209,21 @@ int cdcx_decode_batch_device(cdcx_ctx* ctx, int32_t n_ranks, const uint8_t* d_in
                              const int32_t* d_keys, int64_t n_keys,
                              const int32_t** d_rec_out, int64_t* n_rec_out,
                              const int32_t** d_perm, void* stream);
+
+/* After cdcx_decode_batch_device of n_ranks files: where each rank's part of *d_rec_out and
+ * *d_perm begins (host arrays [n_ranks + 1]; records, and int32 perm entries = matched
+ * events; entry n_ranks = the totals). */
+int cdcx_decode_rank_offsets(cdcx_ctx* ctx, int32_t n_ranks, int64_t* rec_off, int64_t* perm_off);
+
+/* Round-trip check on the device (the size-independent parity property of the batch path;
+ * no counterpart in the reference, whose tests compare validation hashes after replay,
+ * rempi_recorder.cpp:47-79).  Call right after cdcx_encode_batch_device(d_rec, ...) followed by
+ * cdcx_decode_batch_device of its files with its sorted keys on the same context: every
+ * decoded record is compared with the input record it must reproduce (per chunk, per table,
+ * observed order; decoded-record definition ii).  *mismatches = records that differ.
+ * CDCX_ERR_ARG when the trace merges consecutive polls of one table (records are then not
+ * 1:1; the synthetic workload never does). */
+int cdcx_verify_roundtrip_device(cdcx_ctx* ctx, const int32_t* d_rec, int64_t* mismatches, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Replay-side streaming decode (config 5).  Replaces one

@@ -362,6 +362,10 @@ int decode_perm(const u64* ids, const u64* delays, int64_t P, int64_t M, int32_t
     int64_t id = (int64_t)(int)ids[k];
     int64_t dl = (int64_t)(int)delays[k];
     if (id < 0 || id >= M) return ORACLE_ERR_CORRUPT;
+    // The encoder never writes a delay that walks more than once round the list; the
+    // reference would keep stepping through the std::list sentinel.  Treated as corrupt so
+    // that damaged files cost O(M) per pair at most.
+    if (dl > M || dl < -M) return ORACLE_ERR_CORRUPT;
     int64_t at = nx[id];
     nx[pv[id]] = nx[id];
     pv[nx[id]] = pv[id];

@@ -54,6 +54,22 @@ class ReplayStats(ctypes.Structure):
                 ("device_s", ctypes.c_double), ("dump_s", ctypes.c_double), ("sink_s", ctypes.c_double)]
 
 
+class Table(ctypes.Structure):
+    """cdcx_table: one decoded matching-set table of a chunk (flat arrays)."""
+    _fields_ = [("set_id", ctypes.c_int32), ("count", ctypes.c_int32),
+                ("n_epoch", ctypes.c_size_t), ("epoch_rank", P(ctypes.c_uint64)), ("epoch_clock", P(ctypes.c_uint64)),
+                ("n_with_previous", ctypes.c_size_t), ("with_previous", P(ctypes.c_uint64)),
+                ("n_matched_index", ctypes.c_size_t), ("matched_index", P(ctypes.c_uint64)),
+                ("n_unmatched", ctypes.c_size_t), ("unmatched_id", P(ctypes.c_uint64)),
+                ("unmatched_count", P(ctypes.c_uint64)),
+                ("n_pairs", ctypes.c_size_t), ("ids", P(ctypes.c_uint64)), ("delays", P(ctypes.c_uint64)),
+                ("perm", P(ctypes.c_int32))]
+
+
+class Tables(ctypes.Structure):
+    _fields_ = [("n_tables", ctypes.c_size_t), ("tables", P(Table))]
+
+
 _REPLAY_SINK = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.c_int32, _i64p, ctypes.c_size_t)
 
 _SIGNATURES = {
@@ -72,7 +88,12 @@ _SIGNATURES = {
     "cdcx_batch_sorted_keys": ([_vp, P(_vp), _i64p], ctypes.c_int),
     "cdcx_decode_stream": ([_vp, _u8p, ctypes.c_size_t, P(_u8p), P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_reconstruct_stream": ([_vp, _u8p, ctypes.c_size_t, _i32p, ctypes.c_size_t, P(_i32p), P(ctypes.c_size_t)], ctypes.c_int),
+    "cdcx_decode_chunk": ([_vp, _u8p, ctypes.c_size_t, P(Tables)], ctypes.c_int),
+    "cdcx_reconstruct_chunk": ([_vp, _u8p, ctypes.c_size_t, _i32p, ctypes.c_size_t, P(_i32p), P(ctypes.c_size_t)], ctypes.c_int),
+    "cdcx_footer": ([_i32p, ctypes.c_size_t, _u8p, P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_decode_batch_device": ([_vp, ctypes.c_int32, _vp, _i64p, _i64p, _vp, ctypes.c_int64, P(_vp), _i64p, P(_vp), _vp], ctypes.c_int),
+    "cdcx_decode_rank_offsets": ([_vp, ctypes.c_int32, _i64p, _i64p], ctypes.c_int),
+    "cdcx_verify_roundtrip_device": ([_vp, _vp, _i64p, _vp], ctypes.c_int),
     "cdcx_replay_decode_files": ([P(_vp), ctypes.c_int32, ctypes.c_int32, P(ctypes.c_char_p), ctypes.c_int64,
                                   _REPLAY_SINK, _vp, P(ReplayStats)], ctypes.c_int),
     "cdcx_generate_device": ([_vp, P(GenParams), ctypes.c_int32, ctypes.c_int32, P(_vp), _i64p, _vp], ctypes.c_int),
@@ -148,6 +169,21 @@ def gzip_file(data: bytes) -> bytes:
 def gunzip_file(data: bytes) -> bytes:
     """A REMPI_GZIP=1 CDC rank file -> the plain one (cdcx_gunzip_file; host only, no GPU)."""
     return _zlib_stage(lib().cdcx_gunzip_file, data)
+
+
+def footer(epoch_ranks) -> bytes:
+    """write_footer's bytes for the epoch ranks inserted in this order (cdcx_footer; host only)."""
+    L = lib()
+    r = np.ascontiguousarray(epoch_ranks, dtype=np.int32)
+    n = ctypes.c_size_t(0)
+    rc = L.cdcx_footer(_ptr(r, ctypes.c_int32), r.size, None, ctypes.byref(n))
+    if rc:
+        raise CdcxError(rc, "footer size")
+    out = np.zeros(n.value, np.uint8)
+    rc = L.cdcx_footer(_ptr(r, ctypes.c_int32), r.size, _ptr(out, ctypes.c_uint8), ctypes.byref(n))
+    if rc:
+        raise CdcxError(rc, "footer")
+    return out[: n.value].tobytes()
 
 
 class Context:
@@ -234,6 +270,44 @@ class Context:
         L.cdcx_free(out)
         return d
 
+    def decode_chunk(self, payload: bytes):
+        """One chunk payload -> list of dicts (ascending set id) with the decoded table fields
+        (cdcx_decode_chunk)."""
+        L = lib()
+        buf = np.frombuffer(bytes(payload), dtype=np.uint8).copy() if payload else np.zeros(1, np.uint8)
+        t = Tables()
+        self._check(L.cdcx_decode_chunk(self._c, _ptr(buf, ctypes.c_uint8), len(payload), ctypes.byref(t)), "decode_chunk")
+
+        def arr(ptr, n, dt):
+            return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt).copy() if n else np.zeros(0, dt)
+
+        out = []
+        for i in range(t.n_tables):
+            x = t.tables[i]
+            out.append({"set_id": x.set_id, "count": x.count,
+                        "epoch_rank": arr(x.epoch_rank, x.n_epoch, np.int64),
+                        "epoch_clock": arr(x.epoch_clock, x.n_epoch, np.int64),
+                        "with_previous": arr(x.with_previous, x.n_with_previous, np.int64),
+                        "matched_index": arr(x.matched_index, x.n_matched_index, np.int64),
+                        "unmatched_id": arr(x.unmatched_id, x.n_unmatched, np.int64),
+                        "unmatched_count": arr(x.unmatched_count, x.n_unmatched, np.int64),
+                        "ids": arr(x.ids, x.n_pairs, np.int64), "delays": arr(x.delays, x.n_pairs, np.int64),
+                        "perm": arr(x.perm, x.count, np.int32)})
+        L.cdcx_free(t.tables)
+        return out
+
+    def reconstruct_chunk(self, payload: bytes, keys: np.ndarray) -> np.ndarray:
+        L = lib()
+        buf = np.frombuffer(bytes(payload), dtype=np.uint8).copy()
+        k = np.ascontiguousarray(keys, dtype=np.int32).reshape(-1, 2)
+        out = _i32p()
+        n = ctypes.c_size_t()
+        self._check(L.cdcx_reconstruct_chunk(self._c, _ptr(buf, ctypes.c_uint8), buf.size, _ptr(k, ctypes.c_int32),
+                                             k.shape[0], ctypes.byref(out), ctypes.byref(n)), "reconstruct_chunk")
+        arr = np.ctypeslib.as_array(out, shape=(max(n.value, 1) * 8,))[: 8 * n.value].copy().reshape(-1, 8)
+        L.cdcx_free(out)
+        return arr
+
     def reconstruct_stream(self, data: bytes, keys: np.ndarray) -> np.ndarray:
         L = lib()
         buf = np.frombuffer(data, dtype=np.uint8).copy()
@@ -289,6 +363,21 @@ class Context:
                                                d_keys, n_keys, ctypes.byref(dr), ctypes.byref(nr), ctypes.byref(dp),
                                                stream), "decode_batch_device")
         return dr.value, nr.value, dp.value
+
+    def decode_rank_offsets(self, n_ranks: int):
+        """After decode_batch_device: (record offsets, perm offsets) of each rank, n_ranks + 1 each."""
+        ro = np.zeros(n_ranks + 1, np.int64)
+        po = np.zeros(n_ranks + 1, np.int64)
+        self._check(lib().cdcx_decode_rank_offsets(self._c, n_ranks, _ptr(ro, ctypes.c_int64), _ptr(po, ctypes.c_int64)),
+                    "decode_rank_offsets")
+        return ro, po
+
+    def verify_roundtrip_device(self, d_rec: int, stream=None) -> int:
+        """After encode_batch_device(d_rec) + decode_batch_device of its files and keys: the
+        number of decoded records that differ from their input record (device-side check)."""
+        n = ctypes.c_int64(-1)
+        self._check(lib().cdcx_verify_roundtrip_device(self._c, d_rec, ctypes.byref(n), stream), "verify_roundtrip_device")
+        return n.value
 
     # -- profiling -----------------------------------------------------------------------
     def set_profiling(self, on: bool):

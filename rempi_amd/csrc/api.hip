@@ -33,7 +33,7 @@ enum KernelId {
   K_SET_PRESENCE, K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_INC0, K_TILE_SUM, K_RANK_SCAN, K_TILE_P0,
   K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_WINDOW_RANK, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_G16, K_CHAIN_G64, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
   K_WRITE_UNITS, K_CHUNK_HEADERS, K_FOOTER_ORDER, K_FOOTER_WRITE, K_WRITE_KEYS,
-  K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS, K_DEC_PACK,
+  K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS, K_DEC_PACK, K_VERIFY,
   K_GEN_TILE_SUMS, K_GEN_RANK_SCAN, K_GEN_FRAMES, K_GEN_AKEYS, K_GEN_ARRIVAL, K_GEN_RECORDS,
   K_COUNT
 };
@@ -41,7 +41,7 @@ const char* kKernelNames[K_COUNT] = {
   "k_set_presence", "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_inc0", "k_tile_sum", "k_rank_scan",
   "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_window_rank", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
-  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records", "k_dec_pack_tables",
+  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records", "k_dec_pack_tables", "k_verify_roundtrip",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
 
 struct HipError {
@@ -106,6 +106,8 @@ struct cdcx_ctx {
   uint8_t* d_out = nullptr;
   int2* d_keys = nullptr;
   int64_t n_keys = 0;
+  std::vector<Unit> enc_units;       // units of the last encode (file order)
+  std::vector<int64_t> enc_rec_off;  // record offsets of its ranks
   // results of the last decode
   std::vector<DUnit> dunits;
   std::vector<DChunk> dchunks;
@@ -597,6 +599,8 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   c->d_out = d_out;
   c->d_keys = d_keys;
   c->n_keys = key_run;
+  c->enc_units = units;
+  c->enc_rec_off = rec_off;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1075,6 +1079,161 @@ int cdcx_decode_stream(cdcx_ctx* c, const uint8_t* in, size_t len, uint8_t** dum
   });
 }
 
+}  // extern "C"
+
+namespace {
+
+// One chunk payload as a one-chunk rank file image in device memory (length word, payload,
+// separator, empty footer), so that the batch decoder's framing walk applies unchanged.
+// The payload starts at byte 8 of the image.
+uint8_t* upload_chunk_image(cdcx_ctx* c, const uint8_t* payload, size_t len, int64_t* image_len, hipStream_t s) {
+  if (len & 7) throw CdcxError{CDCX_ERR_CORRUPT, "chunk payload is not a multiple of 8 bytes"};
+  if (len == 0) throw CdcxError{CDCX_ERR_CORRUPT, "empty chunk payload (0 is the footer separator)"};
+  const uint64_t head = len;
+  const uint64_t tail[3] = {0, 0, 0};  // separator, footer rank count 0, int32 map length 0 (+ pad)
+  uint8_t* d = c->buf<uint8_t>("h_file", len + 32);
+  HIPCHK(hipMemcpyAsync(d, &head, 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d + 8, payload, len, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d + 8 + len, tail, 20, hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));  // head/tail live on this frame
+  *image_len = (int64_t)len + 28;
+  return d;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cdcx_decode_chunk(cdcx_ctx* c, const uint8_t* payload, size_t len, cdcx_tables* out) {
+  if (!c || !payload || !out) return CDCX_ERR_ARG;
+  out->n_tables = 0;
+  out->tables = nullptr;
+  return guarded(c, [&] {
+    std::vector<uint8_t> plain;
+    if (c->gzip) {
+      plain = inflate_payload(payload, len);
+      payload = plain.data();
+      len = plain.size();
+    }
+    hipStream_t s = c->stream;
+    int64_t L = 0;
+    uint8_t* d = upload_chunk_image(c, payload, len, &L, s);
+    decode_batch(c, 1, d, {0}, {L}, nullptr, 0, false, s);
+    const DecodedTables t = download_tables(c, s);
+    // test_tables_map: ascending set id, the last table of an id wins
+    std::map<int32_t, int32_t> bysid;
+    for (int32_t q = 0; q < (int32_t)c->dunits.size(); q++) bysid[c->dunits[q].set_id] = q;
+    size_t words = 0, perms = 0;
+    for (auto& kv : bysid) {
+      const DUnit& u = c->dunits[kv.second];
+      words += 2 * (size_t)u.S + u.W + u.Mi + 2 * (size_t)(u.Uc > 0 ? u.U : 0) + 2 * (size_t)u.P;
+      perms += (size_t)u.M;
+    }
+    const size_t head_bytes = align_up((int64_t)(bysid.size() * sizeof(cdcx_table)), 16);
+    uint8_t* block = static_cast<uint8_t*>(malloc(std::max<size_t>(head_bytes + 8 * words + 4 * perms, 16)));
+    if (!block) throw std::bad_alloc();
+    cdcx_table* tabs = reinterpret_cast<cdcx_table*>(block);
+    uint64_t* w = reinterpret_cast<uint64_t*>(block + head_bytes);
+    int32_t* pm = reinterpret_cast<int32_t*>(block + head_bytes + 8 * words);
+    auto put = [&](const void* src, size_t n) {
+      uint64_t* at = w;
+      if (n) memcpy(w, src, 8 * n);
+      w += n;
+      return at;
+    };
+    size_t k = 0;
+    for (auto& kv : bysid) {
+      const DUnit& u = c->dunits[kv.second];
+      const uint8_t* in = payload - 8;  // section offsets are relative to the image
+      const uint64_t* wpd = t.pk + t.pk_off[kv.second];
+      const size_t U = u.Uc > 0 ? (size_t)u.U : 0;
+      const uint64_t* uidd = wpd + u.W;
+      const uint64_t* idd = uidd + U;
+      const uint64_t* dld = idd + u.P;
+      cdcx_table& o = tabs[k++];
+      o.set_id = u.set_id;
+      o.count = u.M;
+      o.n_epoch = (size_t)u.S;
+      o.epoch_rank = put(in + u.ep_off, u.S);
+      o.epoch_clock = put(in + u.ep_off + 8ll * u.S, u.S);
+      o.n_with_previous = (size_t)u.W;
+      o.with_previous = put(wpd, u.W);
+      o.n_matched_index = (size_t)u.Mi;
+      o.matched_index = put(in + u.mi_off, u.Mi);
+      o.n_unmatched = U;
+      o.unmatched_id = put(uidd, U);
+      o.unmatched_count = put(in + u.ucnt_off, U);
+      o.n_pairs = (size_t)u.P;
+      o.ids = put(idd, u.P);
+      o.delays = put(dld, u.P);
+      o.perm = pm;
+      if (u.M) memcpy(pm, t.perm + u.key_off, 4 * (size_t)u.M);
+      pm += u.M;
+    }
+    out->n_tables = bysid.size();
+    out->tables = tabs;
+  });
+}
+
+int cdcx_reconstruct_chunk(cdcx_ctx* c, const uint8_t* payload, size_t len, const int32_t* keys, size_t n_keys,
+                           int32_t** rec8, size_t* n_out) {
+  if (!c || !payload || (n_keys && !keys) || !rec8 || !n_out) return CDCX_ERR_ARG;
+  return guarded(c, [&] {
+    std::vector<uint8_t> plain;
+    if (c->gzip) {
+      plain = inflate_payload(payload, len);
+      payload = plain.data();
+      len = plain.size();
+    }
+    hipStream_t s = c->stream;
+    int64_t L = 0;
+    uint8_t* d = upload_chunk_image(c, payload, len, &L, s);
+    int2* dk = c->buf<int2>("h_keys", n_keys);
+    if (n_keys) HIPCHK(hipMemcpyAsync(dk, keys, 8 * n_keys, hipMemcpyHostToDevice, s));
+    decode_batch(c, 1, d, {0}, {L}, dk, (int64_t)n_keys, true, s);
+    std::vector<int32_t> r = c->download(c->d_rec_out, 8 * c->n_rec_out, s);
+    *rec8 = host_copy(r);
+    *n_out = (size_t)c->n_rec_out;
+  });
+}
+
+int cdcx_footer(const int32_t* epoch_ranks, size_t n_in, uint8_t* out, size_t* len) {
+  if ((n_in && !epoch_ranks) || !len || n_in > (size_t)INT32_MAX - 1) return CDCX_ERR_ARG;
+  try {
+    // std::unordered_set<int>: identity hash of the sign-extended int (hash_order.h)
+    std::vector<uint64_t> key(n_in + 1);
+    std::vector<int32_t> next(n_in + 1), bucket(hash_bucket_capacity(n_in) + 1);
+    HashOrder h;
+    h.init(key.data(), next.data(), bucket.data());
+    for (size_t i = 0; i < n_in; i++) {
+      const uint64_t k = (uint64_t)(int64_t)epoch_ranks[i];
+      if (!h.contains(k)) h.insert_new(k);
+    }
+    const size_t need = 8 + 8 + 4 * (size_t)h.size + 4;
+    if (out) {
+      if (*len < need) {
+        *len = need;
+        return CDCX_ERR_ARG;
+      }
+      uint64_t v = 0;
+      memcpy(out, &v, 8);
+      v = (uint64_t)h.size;
+      memcpy(out + 8, &v, 8);
+      size_t q = 16;
+      for (int32_t p = h.head; p != -1; p = h.next[p], q += 4) {
+        const int32_t r = (int32_t)(int64_t)h.key[p];
+        memcpy(out + q, &r, 4);
+      }
+      const int32_t zero = 0;
+      memcpy(out + q, &zero, 4);
+    }
+    *len = need;
+    return CDCX_OK;
+  } catch (const std::bad_alloc&) {
+    return CDCX_ERR_NOMEM;
+  }
+}
+
 int cdcx_reconstruct_stream(cdcx_ctx* c, const uint8_t* in, size_t len, const int32_t* keys, size_t n_keys,
                             int32_t** rec8, size_t* n_out) {
   if (!c || (len && !in) || (n_keys && !keys) || !rec8 || !n_out) return CDCX_ERR_ARG;
@@ -1137,6 +1296,55 @@ int cdcx_decode_batch_device(cdcx_ctx* c, int32_t n_ranks, const uint8_t* d_in, 
     *d_rec_out = c->d_rec_out;
     *n_rec_out = c->n_rec_out;
     *d_perm = c->d_perm;
+  });
+}
+
+int cdcx_decode_rank_offsets(cdcx_ctx* c, int32_t n_ranks, int64_t* rec_off, int64_t* perm_off) {
+  if (!c || n_ranks < 0 || !rec_off || !perm_off || (size_t)n_ranks + 1 != c->dcbase.size()) return CDCX_ERR_ARG;
+  const size_t NU = c->dunits.size(), C = c->dfirst_unit.size();
+  int64_t rec_end = 0, perm_end = 0;
+  if (NU) {
+    const DUnit& u = c->dunits[NU - 1];
+    rec_end = u.rec_off + u.M + (u.Uc > 0 ? u.U : 0);
+    perm_end = u.key_off + u.M;
+  }
+  for (int32_t r = 0; r <= n_ranks; r++) {
+    // first unit of the first chunk of rank r or of any later rank (chunks may hold no table)
+    size_t k = (size_t)c->dcbase[r];
+    while (k < C && c->dnunits[k] == 0) k++;
+    const bool have = k < C;
+    rec_off[r] = have ? c->dunits[c->dfirst_unit[k]].rec_off : rec_end;
+    perm_off[r] = have ? c->dunits[c->dfirst_unit[k]].key_off : perm_end;
+  }
+  return CDCX_OK;
+}
+
+int cdcx_verify_roundtrip_device(cdcx_ctx* c, const int32_t* d_rec, int64_t* mismatches, void* stream) {
+  if (!c || !d_rec || !mismatches) return CDCX_ERR_ARG;
+  return guarded(c, [&] {
+    hipStream_t s = (hipStream_t)stream;
+    const int32_t NU = (int32_t)c->enc_units.size();
+    if (c->dunits.size() != c->enc_units.size())
+      throw CdcxError{CDCX_ERR_ARG, "the last decode does not hold the units of the last encode"};
+    std::vector<int64_t> dec_off(NU + 1, 0);
+    for (int32_t q = 0; q < NU; q++) {
+      const Unit& u = c->enc_units[q];
+      const DUnit& d = c->dunits[q];
+      if (u.M + u.U != u.n) throw CdcxError{CDCX_ERR_ARG, "trace merges consecutive polls of a table: records are not 1:1"};
+      if (d.M != u.M || d.set_id != u.set_id || d.rec_off != dec_off[q])
+        throw CdcxError{CDCX_ERR_CORRUPT, "decoded unit " + std::to_string(q) + " does not match the encoder's unit"};
+      dec_off[q + 1] = dec_off[q] + u.n;
+    }
+    if (dec_off[NU] != c->n_rec_out || !c->d_rec_out)
+      throw CdcxError{CDCX_ERR_ARG, "the last decode did not reconstruct records"};
+    int64_t* d_dec_off = c->upload("v_dec_off", dec_off, s);
+    int64_t* d_rec_off = c->upload("rec_off", c->enc_rec_off, s);
+    unsigned long long* d_bad = c->buf<unsigned long long>("v_bad", 1);
+    HIPCHK(hipMemsetAsync(d_bad, 0, 8, s));
+    c->launch(K_VERIFY, k_verify_roundtrip, dim3(NU), dim3(256), s, (const Unit*)c->buf<Unit>("units", 0),
+              (const int64_t*)d_dec_off, (const int64_t*)d_rec_off, (const int32_t*)c->buf<int32_t>("t2s", 0),
+              reinterpret_cast<const int4*>(d_rec), reinterpret_cast<const int4*>(c->d_rec_out), d_bad);
+    *mismatches = (int64_t)c->download(d_bad, 1, s)[0];
   });
 }
 

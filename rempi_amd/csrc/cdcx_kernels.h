@@ -82,6 +82,8 @@ template <int K>
 __global__ void k_dec_perm_window(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
 __global__ void k_dec_records(const DUnit*, const int2*, const uint8_t*, const int32_t*, const uint8_t*, const uint64_t*,
                               const int2*, int4*);
+__global__ void k_verify_roundtrip(const Unit*, const int64_t*, const int64_t*, const int32_t*, const int4*, const int4*,
+                                   unsigned long long*);
 __global__ void k_dec_pack_tables(const DUnit*, const int64_t*, const uint64_t*, const uint64_t*, const uint64_t*,
                                   const uint64_t*, uint64_t*);
 

@@ -103,7 +103,12 @@ __device__ bool walk_units(const uint8_t* __restrict__ in, const DChunk& c, int3
     u.pair_off = q + 8;
     q += 8 + (int64_t)psz;
     if (q > end) return false;
-    if (u.M < 0 || u.P > u.M || u.W > u.M || (u.Uc > 0 && u.Uc < u.U)) return false;
+    // Every per-unit scratch row holds M + 1 words: the sections that are expanded into one
+    // (with_previous, unmatched ids, pairs) must fit it, and the sections indexed by matched
+    // row or run (matched_index, unmatched counts) must cover what the later kernels read.
+    if (u.M < 0 || u.P > u.M || u.W > u.M || (int64_t)u.U > (int64_t)u.M + 1 || (u.Uc > 0 && u.Uc != u.U) ||
+        (u.Mi > 0 && u.Mi != u.M))
+      return false;
     if (units) units[first_unit + k] = u;
     k++;
   }
@@ -681,10 +686,39 @@ __global__ void __launch_bounds__(256) k_dec_records(const DUnit* __restrict__ u
     const int32_t i = i0 + r;
     const int64_t at = u.rec_off + i + mk[r];
     const int2 k = keys[u.key_off + cinv[u.key_off + i]];
-    const int32_t idx = (int32_t)ld_u64(in + u.mi_off + 8ll * i);
+    const int32_t idx = (u.Mi > 0) ? (int32_t)ld_u64(in + u.mi_off + 8ll * i) : 0;  // Mi is M or 0 (rep files)
     rec[2 * at] = make_int4(1, 2, 1, k.x);
     rec[2 * at + 1] = make_int4(wnf[u.wbase + i], idx, k.y, u.set_id);
   }
+}
+
+// Round-trip check on the device: record i of encoder unit u's T-order range is input record
+// rec_off[rank] + t2s[a + i]; after encode + decode of the same batch it must reappear as
+// decoded record dec_off[u] + i with the fields the replay side can rebuild (matched:
+// count 1, type 2, flag 1, source, with_next as 0/1, index, clock, set; unmatched poll: count,
+// type 2, set, everything else 0).  Holds when no two polls of a table were merged
+// (M + U == n for every unit); the host checks that before launching.
+__global__ void __launch_bounds__(256) k_verify_roundtrip(const Unit* __restrict__ units, const int64_t* __restrict__ dec_off,
+                                                          const int64_t* __restrict__ rec_off,
+                                                          const int32_t* __restrict__ t2s, const int4* __restrict__ rec_in,
+                                                          const int4* __restrict__ rec_out,
+                                                          unsigned long long* __restrict__ bad) {
+  const Unit u = units[blockIdx.x];
+  const int64_t rb = rec_off[u.rank], ob = dec_off[blockIdx.x];
+  int32_t nbad = 0;
+  for (int32_t i = threadIdx.x; i < u.n; i += 256) {
+    const int64_t g = rb + t2s[u.a + i];
+    const int4 lo = rec_in[2 * g], hi = rec_in[2 * g + 1];
+    const int4 a = rec_out[2 * (ob + i)], b = rec_out[2 * (ob + i) + 1];
+    const bool m = lo.z == 1;
+    const int4 wa = m ? make_int4(1, 2, 1, lo.w) : make_int4(lo.x, 2, 0, 0);
+    const int4 wb = m ? make_int4(hi.x != 0 ? 1 : 0, hi.y, hi.z, hi.w) : make_int4(0, 0, 0, hi.w);
+    if (a.x != wa.x || a.y != wa.y || a.z != wa.z || a.w != wa.w || b.x != wb.x || b.y != wb.y || b.z != wb.z ||
+        b.w != wb.w)
+      nbad++;
+  }
+  nbad = wave_reduce(nbad, OpAdd());
+  if (lane_id() == 0 && nbad) atomicAdd(bad, (unsigned long long)nbad);
 }
 
 }  // namespace cdcx

@@ -85,44 +85,76 @@ std::vector<uint8_t> frame(const std::vector<std::vector<uint8_t>>& z, const uin
 
 }  // namespace
 
+// zlib counts input and output in uInt: larger buffers are fed in pieces (the stream does not
+// depend on how its input or output space is split).
+constexpr size_t kZPiece = (size_t)1 << 30;
+
 std::vector<uint8_t> deflate_payload(const uint8_t* p, size_t n) {
   z_stream s{};
   if (deflateInit(&s, Z_DEFAULT_COMPRESSION) != Z_OK) throw GzipError{"deflateInit failed"};
-  std::vector<uint8_t> out(deflateBound(&s, (uLong)n));
-  s.next_in = const_cast<Bytef*>(p);
-  s.avail_in = (uInt)n;
-  s.next_out = out.data();
-  s.avail_out = (uInt)out.size();
-  const int rc = deflate(&s, Z_FINISH);
-  out.resize(out.size() - s.avail_out);
+  // deflateBound takes a uLong (64-bit here); add the per-piece slack of stored blocks
+  std::vector<uint8_t> out((size_t)deflateBound(&s, (uLong)n) + 64);
+  size_t in_pos = 0, out_pos = 0;
+  int rc = Z_OK;
+  do {
+    const size_t take = std::min(kZPiece, n - in_pos);
+    s.next_in = const_cast<Bytef*>(p + in_pos);
+    s.avail_in = (uInt)take;
+    in_pos += take;
+    const int flush = (in_pos == n) ? Z_FINISH : Z_NO_FLUSH;
+    do {
+      const size_t room = std::min(kZPiece, out.size() - out_pos);
+      if (room == 0) {
+        deflateEnd(&s);
+        throw GzipError{"deflate output exceeds deflateBound"};
+      }
+      s.next_out = out.data() + out_pos;
+      s.avail_out = (uInt)room;
+      rc = deflate(&s, flush);
+      out_pos += room - s.avail_out;
+      if (rc == Z_STREAM_ERROR) break;
+    } while (s.avail_out == 0 && rc != Z_STREAM_END);
+    if (rc == Z_STREAM_ERROR) break;
+  } while (in_pos < n);
   deflateEnd(&s);
   if (rc != Z_STREAM_END) throw GzipError{"deflate did not finish"};
+  out.resize(out_pos);
   return out;
 }
 
+// One chunk = exactly one zlib stream (rempi_encoder_cdc.cpp:960-978 inflates the whole
+// chunk): input that ends inside the stream, or bytes left after its end, are corrupt.
 std::vector<uint8_t> inflate_payload(const uint8_t* p, size_t n) {
   z_stream s{};
   if (inflateInit(&s) != Z_OK) throw GzipError{"inflateInit failed"};
   std::vector<uint8_t> out(std::max<size_t>(4 * n, 4096));
-  s.next_in = const_cast<Bytef*>(p);
-  s.avail_in = (uInt)n;
-  int rc;
+  size_t in_pos = 0, out_pos = 0;
+  int rc = Z_OK;
   while (true) {
-    s.next_out = out.data() + s.total_out;
-    s.avail_out = (uInt)(out.size() - s.total_out);
+    if (s.avail_in == 0 && in_pos < n) {
+      const size_t take = std::min(kZPiece, n - in_pos);
+      s.next_in = const_cast<Bytef*>(p + in_pos);
+      s.avail_in = (uInt)take;
+      in_pos += take;
+    }
+    if (out_pos == out.size()) out.resize(out.size() * 2);
+    const size_t room = std::min(kZPiece, out.size() - out_pos);
+    s.next_out = out.data() + out_pos;
+    s.avail_out = (uInt)room;
     rc = inflate(&s, Z_NO_FLUSH);
+    out_pos += room - s.avail_out;
     if (rc == Z_STREAM_END) break;
     if (rc != Z_OK && rc != Z_BUF_ERROR) break;
-    if (s.avail_out == 0) {
-      out.resize(out.size() * 2);
-    } else if (s.avail_in == 0) {
+    if (s.avail_out != 0 && s.avail_in == 0 && in_pos == n) {
       rc = Z_DATA_ERROR;  // input ended inside the stream
       break;
     }
   }
-  out.resize(s.total_out);
+  const bool trailing = (rc == Z_STREAM_END) && (s.avail_in != 0 || in_pos != n);
   inflateEnd(&s);
   if (rc != Z_STREAM_END) throw GzipError{"corrupt zlib chunk"};
+  if (trailing) throw GzipError{"bytes after the end of a chunk's zlib stream"};
+  out.resize(out_pos);
   return out;
 }
 

@@ -1,23 +1,60 @@
-"""Multi-GPU layout of the CDC batch path: rank traces are independent, so
-GPUs take contiguous blocks of ranks and exchange nothing on the data path.  The only
-collective is the end-of-run reduction of counters (sum) and elapsed time (max), over RCCL
-on the GPU box (`nccl` backend) and gloo in the CPU tests.  bench.py uses these helpers."""
+"""Multi-GPU layout of the CDC batch path: rank traces are independent, so each GPU takes one
+contiguous block of the job's ranks and exchanges nothing on the data path.  Rank r of an
+R-rank job goes to GPU floor(r * G / R); a GPU walks its block in batches that fit HBM.  The
+only collective is the end-of-run reduction of counters (sum) and elapsed time (max), over
+RCCL on the GPU box (`nccl` backend) and gloo in the CPU tests.  bench.py uses these helpers."""
 from __future__ import annotations
 
 import numpy as np
 
 
-def shard(world: int, n_gpus: int, gpu: int, per_gpu: int) -> tuple[int, int]:
-    """First rank and rank count of GPU `gpu`: block [gpu*per_gpu, (gpu+1)*per_gpu) of the
-    job's ranks (wrapping past `world`, so a weak-scaling run of any size keeps per-GPU work
-    fixed)."""
-    if n_gpus < 1 or not 0 <= gpu < n_gpus or per_gpu < 1 or world < 1:
+def gpu_of_rank(rank: int, world: int, n_gpus: int) -> int:
+    """floor(rank * G / R): the GPU that processes `rank`'s trace."""
+    return rank * n_gpus // world
+
+
+def block(world: int, n_gpus: int, gpu: int) -> tuple[int, int]:
+    """(first rank, rank count) of GPU `gpu`: the ranks r with floor(r * G / R) == gpu, i.e.
+    [ceil(gpu * R / G), ceil((gpu + 1) * R / G)).  The blocks of all GPUs partition [0, R)."""
+    if n_gpus < 1 or not 0 <= gpu < n_gpus or world < 1:
         raise ValueError("bad shard request")
-    return (gpu * per_gpu) % world, per_gpu
+    lo = -(-gpu * world // n_gpus)
+    hi = -(-(gpu + 1) * world // n_gpus)
+    return lo, hi - lo
+
+
+def check_cover(world: int, n_gpus: int) -> None:
+    """Every rank of the job lies in exactly one GPU's block, and in the block of its GPU."""
+    nxt = 0
+    for g in range(n_gpus):
+        first, n = block(world, n_gpus, g)
+        if first != nxt:
+            raise AssertionError(f"GPU {g} starts at rank {first}, expected {nxt}")
+        if n and (gpu_of_rank(first, world, n_gpus) != g or gpu_of_rank(first + n - 1, world, n_gpus) != g):
+            raise AssertionError(f"GPU {g} holds ranks of another GPU")
+        nxt = first + n
+    if nxt != world:
+        raise AssertionError(f"blocks end at rank {nxt}, job has {world}")
+
+
+def batches(first: int, count: int, per_batch: int) -> list[tuple[int, int]]:
+    """Split a GPU's block into the fewest batches of at most `per_batch` resident rank traces,
+    sized evenly (e.g. 128 ranks at 96 per batch -> 64 + 64)."""
+    if per_batch < 1:
+        raise ValueError("per_batch must be positive")
+    if count <= 0:
+        return []
+    nb = -(-count // per_batch)
+    out, at = [], first
+    for i in range(nb):
+        n = count // nb + (1 if i < count % nb else 0)
+        out.append((at, n))
+        at += n
+    return out
 
 
 def lane_sizes(count: int, streams: int) -> list[int]:
-    """Split a GPU's ranks over `streams` in-flight batches (one HIP stream each)."""
+    """Split a batch's ranks over `streams` in-flight lanes (one HIP stream each)."""
     s = max(1, min(streams, count))
     return [count // s + (1 if i < count % s else 0) for i in range(s)]
 

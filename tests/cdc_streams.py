@@ -168,3 +168,72 @@ def expected_table_streams(recs: np.ndarray, max_len: int) -> np.ndarray:
                         out.append([r[0], 2, 0, 0, 0, 0, 0, s])
                     prev_unmatched = True
     return np.array(out, dtype=np.int32).reshape(-1, 8)
+
+
+def chunk_bounds_fast(recs: np.ndarray, max_len: int):
+    """chunk_bounds with array operations per chunk (full-size traces): the length rule of
+    add() (rempi_encoder_cdc.cpp:178-218) as a cumulative sum over a window that is sure to
+    hold the chunk's end."""
+    recs = np.asarray(recs, dtype=np.int32).reshape(-1, 8)
+    n = recs.shape[0]
+    matched = recs[:, 2] == 1
+    out, start = [], 0
+    while start < n:
+        win = max(2 * max_len + 64, 1024)
+        while True:
+            end = min(n, start + win)
+            m = matched[start:end]
+            s = recs[start:end, 7]
+            order = np.argsort(s, kind="stable")
+            so = s[order]
+            prev = np.full(end - start, -1, dtype=np.int64)  # previous record of the same set in the window
+            same = np.zeros(end - start, dtype=bool)
+            same[1:] = so[1:] == so[:-1]
+            prev[order[1:]] = np.where(same[1:], order[:-1], -1)
+            prev_unmatched = np.zeros(end - start, dtype=bool)
+            has = prev >= 0
+            prev_unmatched[has] = ~m[prev[has]]
+            inc = np.where(m, 1, np.where(prev_unmatched, 0, 1))
+            length = np.cumsum(inc)
+            close = np.nonzero((length > max_len) & (recs[start:end, 4] == 0))[0]
+            if close.size:
+                stop = start + int(close[0]) + 1
+                break
+            if end == n:
+                stop = n
+                break
+            win *= 2
+        out.append((start, stop))
+        start = stop
+    return out
+
+
+def expected_table_streams_fast(recs: np.ndarray, max_len: int) -> np.ndarray:
+    """expected_table_streams with array operations (full-size traces)."""
+    recs = np.asarray(recs, dtype=np.int32).reshape(-1, 8)
+    parts = []
+    for a, b in chunk_bounds_fast(recs, max_len):
+        ch = recs[a:b]
+        ch = ch[np.argsort(ch[:, 7], kind="stable")]  # per table, observed order
+        m = ch[:, 2] == 1
+        # an unmatched record continues a run when the record before it (same table) is unmatched
+        cont = np.zeros(ch.shape[0], dtype=bool)
+        cont[1:] = (~m[1:]) & (~m[:-1]) & (ch[1:, 7] == ch[:-1, 7])
+        head = ~cont
+        gid = np.cumsum(head) - 1
+        out = np.zeros((int(head.sum()), 8), dtype=np.int32)
+        hm = m[head]
+        hrec = ch[head]
+        out[:, 1] = 2
+        out[:, 7] = hrec[:, 7]
+        out[hm, 0] = 1
+        out[hm, 2] = 1
+        out[hm, 3] = hrec[hm, 3]
+        out[hm, 4] = (hrec[hm, 4] != 0).astype(np.int32)
+        out[hm, 5] = hrec[hm, 5]
+        out[hm, 6] = hrec[hm, 6]
+        cnt = np.zeros(out.shape[0], dtype=np.int64)
+        np.add.at(cnt, gid[~m], ch[~m, 0].astype(np.int64))
+        out[~hm, 0] = cnt[~hm].astype(np.int32)  # wraps like the reference's int add
+        parts.append(out)
+    return np.concatenate(parts) if parts else np.zeros((0, 8), np.int32)
