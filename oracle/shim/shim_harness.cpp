@@ -123,7 +123,9 @@ int run_batch(const char* list) {
     std::vector<std::string> a;
     for (char* t = strtok(line, " \t\n"); t; t = strtok(NULL, " \t\n")) a.push_back(t);
     if (a.empty()) continue;
-    rempi_encoder_input_format_test_table::all_epoch_rank_uset.clear();  // static: one rank per command
+    // static, one rank per command; a fresh set, since clear() keeps the bucket count and the
+    // footer order follows the buckets
+    std::unordered_set<int>().swap(rempi_encoder_input_format_test_table::all_epoch_rank_uset);
     int rc = 1;
     if (a[0] == "encode" && a.size() >= 4)
       rc = run_encode(a[1].c_str(), a[2].c_str(), atoi(a[3].c_str()), a.size() >= 5 && a[4] == "gzip");

@@ -93,7 +93,7 @@ def test_decode_chunk_rejects_damage():
     d = G.load("kat")
     c = rempi_amd.Context(131072)
     pl = chunks_of(d["rempi"])[0][0]
-    for bad in (pl[:-8], pl + b"\0" * 8, pl[:20] + b"\xff" * 8 + pl[28:]):
+    for bad in (pl[:-8], pl + b"\0" * 8, pl[:8] + b"\xff" * 8 + pl[16:]):
         with pytest.raises(cdcx.CdcxError) as e:
             c.decode_chunk(bad)
         assert e.value.code == 4
