@@ -210,6 +210,24 @@ int cdcx_decode_batch_device(cdcx_ctx* ctx, int32_t n_ranks, const uint8_t* d_in
                              const int32_t** d_rec_out, int64_t* n_rec_out,
                              const int32_t** d_perm, void* stream);
 
+/* The one entry point that allocates nothing.  It has no counterpart in the reference; it is
+ * for callers that cannot allocate device memory: code under HIP graph capture, tight replay
+ * loops, harnesses that forbid hipMalloc.  A variant of cdcx_decode_batch_device (tables
+ * only) for ONE chunk already in device memory: d_payload is the chunk payload (what follows
+ * the size_t length in the file, plain CDC), and d_perm receives the
+ * matched_events_permutated_indices (cdc_prepare_decode_indices, :1301-1386) of the chunk's
+ * tables in file order, concatenated: the same int32 values *d_perm of
+ * cdcx_decode_batch_device holds for that chunk.  *n_perm = entries written (sum of the
+ * tables' counts); perm_capacity = entries d_perm can hold.
+ * All scratch (unit table, pair rows, list links; 7 MiB) is a file-scope device array that
+ * each GPU the library runs on holds until the process ends.  Limits: at most 256 tables and
+ * sum(count + 1) <= 262144 per chunk (REMPI_MAX = 131072 chunks fit), else CDCX_ERR_LIMIT.
+ * Calls no hipMalloc / hipFree; it does wait for the stream once, to read the status.
+ * Every call on a GPU uses that GPU's one array: calls that overlap on one GPU (other
+ * streams, other contexts or threads) race -- serialise them. */
+int cdcx_decode_chunk_perm_static(cdcx_ctx* ctx, const uint8_t* d_payload, size_t len, int32_t* d_perm,
+                                  size_t perm_capacity, int64_t* n_perm, void* stream);
+
 /* After cdcx_decode_batch_device of n_ranks files: where each rank's part of *d_rec_out and
  * *d_perm begins (host arrays [n_ranks + 1]; records, and int32 perm entries = matched
  * events; entry n_ranks = the totals). */

@@ -92,6 +92,7 @@ _SIGNATURES = {
     "cdcx_reconstruct_chunk": ([_vp, _u8p, ctypes.c_size_t, _i32p, ctypes.c_size_t, P(_i32p), P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_footer": ([_i32p, ctypes.c_size_t, _u8p, P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_decode_batch_device": ([_vp, ctypes.c_int32, _vp, _i64p, _i64p, _vp, ctypes.c_int64, P(_vp), _i64p, P(_vp), _vp], ctypes.c_int),
+    "cdcx_decode_chunk_perm_static": ([_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _i64p, _vp], ctypes.c_int),
     "cdcx_decode_rank_offsets": ([_vp, ctypes.c_int32, _i64p, _i64p], ctypes.c_int),
     "cdcx_verify_roundtrip_device": ([_vp, _vp, _i64p, _vp], ctypes.c_int),
     "cdcx_replay_decode_files": ([P(_vp), ctypes.c_int32, ctypes.c_int32, P(ctypes.c_char_p), ctypes.c_int64,
@@ -363,6 +364,13 @@ class Context:
                                                d_keys, n_keys, ctypes.byref(dr), ctypes.byref(nr), ctypes.byref(dp),
                                                stream), "decode_batch_device")
         return dr.value, nr.value, dp.value
+
+    def decode_chunk_perm_static(self, d_payload: int, nbytes: int, d_perm: int, perm_capacity: int, stream=None) -> int:
+        """cdcx_decode_chunk_perm_static: device payload -> device perm; returns the entries written."""
+        n = ctypes.c_int64(-1)
+        self._check(lib().cdcx_decode_chunk_perm_static(self._c, d_payload, nbytes, d_perm, perm_capacity, ctypes.byref(n),
+                                                        stream), "decode_chunk_perm_static")
+        return n.value
 
     def decode_rank_offsets(self, n_ranks: int):
         """After decode_batch_device: (record offsets, perm offsets) of each rank, n_ranks + 1 each."""

@@ -79,8 +79,49 @@ constexpr const char* kAliasWnf = "chain";    // with_next flags       <- chain 
 
 }  // namespace
 
+// ---------------------------------------------------------------------------------------
+// Scratch of the entry point that allocates nothing (cdcx_decode_chunk_perm_static): one
+// file-scope device array per GPU, carved into the unit table, the pair rows and the list
+// links of one chunk.  `scratch` is only a host-side handle: its device address is looked up
+// once per device in cdcx_create (static_scratch_of) and kept; kernels, copies and fills
+// always get that address.
+namespace {
+constexpr int32_t kStaticMaxUnits = 256;          // tables per chunk (matching_set_id < 256)
+constexpr int64_t kStaticMaxRows = 262144;        // sum over the chunk's tables of count + 1
+constexpr size_t kStaticHdrOff = 0;               // int32[64] header
+constexpr size_t kStaticOrderOff = 256;           // int32[kStaticMaxUnits]
+constexpr size_t kStaticUnitsOff = kStaticOrderOff + 4 * kStaticMaxUnits;
+constexpr size_t kStaticIddOff = (kStaticUnitsOff + sizeof(DUnit) * kStaticMaxUnits + 255) / 256 * 256;
+constexpr size_t kStaticDldOff = kStaticIddOff + 8 * kStaticMaxRows;
+constexpr size_t kStaticCinvOff = kStaticDldOff + 8 * kStaticMaxRows;
+constexpr size_t kStaticNxOff = kStaticCinvOff + 4 * kStaticMaxRows;
+constexpr size_t kStaticPvOff = kStaticNxOff + 4 * kStaticMaxRows;
+constexpr size_t kStaticScratchBytes = kStaticPvOff + 4 * kStaticMaxRows;  // ~7.0 MiB
+}  // namespace
+static __device__ __align__(256) unsigned char scratch[kStaticScratchBytes];
+namespace {
+constexpr int kMaxDevices = 64;
+std::mutex g_static_mu;
+unsigned char* g_static_scratch[kMaxDevices] = {};  // device address of `scratch` on each GPU
+
+// Device address of this GPU's copy of `scratch` (the device must be current).
+hipError_t static_scratch_of(int device, unsigned char** out) {
+  std::lock_guard<std::mutex> g(g_static_mu);
+  if (device < 0 || device >= kMaxDevices) return hipErrorInvalidDevice;
+  if (!g_static_scratch[device]) {
+    void* p = nullptr;
+    const hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(scratch));
+    if (e != hipSuccess) return e;
+    g_static_scratch[device] = static_cast<unsigned char*>(p);
+  }
+  *out = g_static_scratch[device];
+  return hipSuccess;
+}
+}  // namespace
+
 struct cdcx_ctx {
   int device = 0;
+  unsigned char* static_scratch = nullptr;  // this device's `scratch` (static_scratch_of)
   int gzip = 0;  // REMPI_GZIP: host-buffer encode/decode apply the zlib stage (gzip_stage.hip)
   bool rep = false;  // REMPI_ENCODE=7: epoch lines only (rempi_encoder_rep.cpp:50-146)
   int64_t max_len = 131072;
@@ -882,6 +923,11 @@ cdcx_ctx* cdcx_create(const cdcx_opts* opts) {
     delete c;
     return nullptr;
   }
+  if (static_scratch_of(c->device, &c->static_scratch) != hipSuccess) {
+    (void)hipGetLastError();
+    delete c;
+    return nullptr;
+  }
   return c;
 }
 
@@ -1297,6 +1343,63 @@ int cdcx_decode_batch_device(cdcx_ctx* c, int32_t n_ranks, const uint8_t* d_in, 
     *n_rec_out = c->n_rec_out;
     *d_perm = c->d_perm;
   });
+}
+
+int cdcx_decode_chunk_perm_static(cdcx_ctx* c, const uint8_t* d_payload, size_t len, int32_t* d_perm,
+                                  size_t perm_capacity, int64_t* n_perm, void* stream) {
+  if (!c || !d_payload || !d_perm || !n_perm) return CDCX_ERR_ARG;
+  *n_perm = 0;
+  if (len == 0 || (len & 7) || len > ((size_t)1 << 40)) {
+    c->err = "chunk payload length must be a positive multiple of 8";
+    return CDCX_ERR_CORRUPT;
+  }
+  // No allocation anywhere below: fixed-size launches over this device's static scratch, one
+  // small D2H of the header at the end.
+  hipStream_t s = (hipStream_t)stream;
+  if (hipSetDevice(c->device) != hipSuccess || !c->static_scratch) {
+    (void)hipGetLastError();
+    c->err = "no static scratch on this device";
+    return CDCX_ERR_HIP;
+  }
+  unsigned char* sc = c->static_scratch;
+  int32_t* hdr = reinterpret_cast<int32_t*>(sc + kStaticHdrOff);
+  int32_t* order = reinterpret_cast<int32_t*>(sc + kStaticOrderOff);
+  DUnit* units = reinterpret_cast<DUnit*>(sc + kStaticUnitsOff);
+  uint64_t* idd = reinterpret_cast<uint64_t*>(sc + kStaticIddOff);
+  uint64_t* dld = reinterpret_cast<uint64_t*>(sc + kStaticDldOff);
+  int32_t* cinv = reinterpret_cast<int32_t*>(sc + kStaticCinvOff);
+  int32_t* nx = reinterpret_cast<int32_t*>(sc + kStaticNxOff);
+  int32_t* pv = reinterpret_cast<int32_t*>(sc + kStaticPvOff);
+  const int64_t cap = (int64_t)std::min<size_t>(perm_capacity, (size_t)kStaticMaxRows);
+  hipLaunchKernelGGL(k_dec_chunk_units, dim3(1), dim3(64), 0, s, d_payload, (int64_t)len, kStaticMaxUnits, kStaticMaxRows, cap,
+                     hdr, order, units);
+  hipLaunchKernelGGL(k_dec_perm_grp, dim3(kStaticMaxUnits / 4), dim3(64), 0, s, units, (const int32_t*)order, kStaticMaxUnits,
+                     d_payload, idd, dld, d_perm, cinv, hdr + 2);
+  hipLaunchKernelGGL(k_dec_perm_window<4>, dim3(kStaticMaxUnits), dim3(64), 0, s, units, kStaticMaxUnits, 1,
+                     (const uint64_t*)idd, (const uint64_t*)dld, d_perm, hdr + 3);
+  hipLaunchKernelGGL(k_dec_perm_lane, dim3(kStaticMaxUnits / 64), dim3(64), 0, s, (const DUnit*)units, kStaticMaxUnits,
+                     (const uint64_t*)idd, (const uint64_t*)dld, nx, pv, d_perm, reinterpret_cast<uint32_t*>(hdr));
+  int32_t h[6] = {0, 0, 0, 0, 0, 0};
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(h, hdr, sizeof(h), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    c->err = std::string("cdcx_decode_chunk_perm_static: ") + hipGetErrorString(e);
+    return CDCX_ERR_HIP;
+  }
+  const uint32_t bits = (uint32_t)h[0];
+  if (bits & (1u << CDCX_ERR_LIMIT)) {
+    c->err = "chunk exceeds the static scratch (sum of count + 1 over its tables > 262144, more than 256 tables, or "
+             "more matched events than perm_capacity)";
+    return CDCX_ERR_LIMIT;
+  }
+  if (bits) {
+    c->err = "Record data is broken";
+    return CDCX_ERR_CORRUPT;
+  }
+  *n_perm = (int64_t)(((uint64_t)(uint32_t)h[5] << 32) | (uint32_t)h[4]);
+  c->err.clear();
+  return CDCX_OK;
 }
 
 int cdcx_decode_rank_offsets(cdcx_ctx* c, int32_t n_ranks, int64_t* rec_off, int64_t* perm_off) {

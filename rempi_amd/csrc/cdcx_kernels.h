@@ -72,6 +72,7 @@ __global__ void k_write_keys(const Unit*, const uint64_t*, int2*);
 __global__ void k_dec_count_chunks(const uint8_t*, const int64_t*, const int64_t*, int32_t, int32_t*, uint32_t*);
 __global__ void k_dec_list_chunks(const uint8_t*, const int64_t*, const int32_t*, const int32_t*, int32_t, DChunk*);
 __global__ void k_dec_units(const uint8_t*, const DChunk*, int32_t, const int32_t*, int32_t*, DUnit*, uint32_t*);
+__global__ void k_dec_chunk_units(const uint8_t*, int64_t, int32_t, int64_t, int64_t, int32_t*, int32_t*, DUnit*);
 __global__ void k_dec_sections(const DUnit*, const uint8_t*, uint64_t*, uint64_t*, uint8_t*, uint32_t*);
 __global__ void k_dec_perm_lane(const DUnit*, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*, int32_t*,
                                 uint32_t*);

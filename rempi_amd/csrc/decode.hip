@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(64) k_dec_list_chunks(const uint8_t* __restric
 
 // Walk the tables of one chunk payload.  When `units` is null only counts.
 __device__ bool walk_units(const uint8_t* __restrict__ in, const DChunk& c, int32_t first_unit, DUnit* units,
-                           int32_t* count) {
+                           int32_t* count, int32_t max_units = INT32_MAX) {
   int64_t q = c.off;
   const int64_t end = c.off + c.len;
   int32_t k = 0;
@@ -109,6 +109,7 @@ __device__ bool walk_units(const uint8_t* __restrict__ in, const DChunk& c, int3
     if (u.M < 0 || u.P > u.M || u.W > u.M || (int64_t)u.U > (int64_t)u.M + 1 || (u.Uc > 0 && u.Uc != u.U) ||
         (u.Mi > 0 && u.Mi != u.M))
       return false;
+    if (k >= max_units) return false;
     if (units) units[first_unit + k] = u;
     k++;
   }
@@ -124,6 +125,56 @@ __global__ void __launch_bounds__(64) k_dec_units(const uint8_t* __restrict__ in
   int32_t k = 0;
   if (!walk_units(in, chunks[c], units ? first_unit[c] : 0, units, &k)) raise_error(err, kErrCorrupt);
   if (nunits) nunits[c] = k;
+}
+
+// One chunk payload at `in` (len bytes), everything on the device: the unit table (at most
+// max_units entries, the rest zeroed so that fixed-size launches over max_units units find
+// empty units), the scratch offsets of each unit, an identity launch order and the header
+// words {error bits, units, window-tier failures, list-tier failures, matched events (2
+// words)}.  A payload whose units need more than max_rows scratch rows (sum of M + 1) or more
+// than perm_capacity permutation entries is refused with the limit bit and an empty table.
+__global__ void __launch_bounds__(64) k_dec_chunk_units(const uint8_t* __restrict__ in, int64_t len, int32_t max_units,
+                                                        int64_t max_rows, int64_t perm_capacity,
+                                                        int32_t* __restrict__ hdr, int32_t* __restrict__ order,
+                                                        DUnit* __restrict__ units) {
+  __shared__ int32_t nu_s;
+  if (threadIdx.x == 0) {
+    int32_t k = 0;
+    uint32_t e = 0;
+    const DChunk c{0, len, 0, 0};
+    if ((len & 7) || len <= 0 || !walk_units(in, c, 0, units, &k, max_units)) {
+      e |= 1u << kErrCorrupt;
+      k = 0;
+    }
+    int64_t wb = 0, ko = 0;
+    for (int32_t q = 0; q < k; q++) {
+      DUnit& u = units[q];
+      u.wbase = wb;
+      u.rec_off = ko + q;  // not used by the permutation kernels
+      u.key_off = ko;
+      u.fb = 0;
+      wb += (int64_t)u.M + 1;
+      ko += u.M;
+    }
+    if (wb > max_rows || ko > perm_capacity) {
+      e |= 1u << kErrLimit;
+      k = 0;
+      ko = 0;
+    }
+    hdr[0] = (int32_t)e;
+    hdr[1] = k;
+    hdr[2] = 0;
+    hdr[3] = 0;
+    hdr[4] = (int32_t)(ko & 0xffffffff);
+    hdr[5] = (int32_t)(ko >> 32);
+    nu_s = k;
+  }
+  __syncthreads();
+  const int32_t nu = nu_s;
+  for (int32_t q = threadIdx.x; q < max_units; q += 64) {
+    order[q] = q;
+    if (q >= nu) units[q] = DUnit{};
+  }
 }
 
 // Inverse LP of one section: x = prefix(prefix(y)) mod 2^64.  Loads either 8-byte words
