@@ -1552,8 +1552,14 @@ extern "C" {
 int cdcx_replay_decode_files(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths,
                              int64_t batch_bytes, cdcx_replay_sink sink, void* user, cdcx_replay_stats* stats) {
   if (!ctxs || n_ctx <= 0 || n_files < 0 || (n_files && !paths) || !sink) return CDCX_ERR_ARG;
-  for (int32_t i = 0; i < n_ctx; i++)
+  for (int32_t i = 0; i < n_ctx; i++) {
     if (!ctxs[i]) return CDCX_ERR_ARG;
+    for (int32_t k = 0; k < i; k++)
+      if (ctxs[k] == ctxs[i]) {  // one worker thread per entry: a context must not be shared
+        ctxs[i]->err = "the same context was passed twice";
+        return CDCX_ERR_ARG;
+      }
+  }
   const auto t0 = std::chrono::steady_clock::now();
   ReplayJob job;
   job.paths = paths;
