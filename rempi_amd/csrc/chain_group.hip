@@ -36,7 +36,7 @@ struct Grp<16> {
   __device__ static __forceinline__ int lane() { return threadIdx.x & 15; }
   __device__ static __forceinline__ int base() { return threadIdx.x & 48; }
   __device__ static __forceinline__ Mask ballot(bool p) {
-    return (Mask)((unsigned long long)__ballot(p) >> base()) & 0xFFFFu;
+    return (Mask)((unsigned long long)__builtin_amdgcn_ballot_w64(p) >> base()) & 0xFFFFu;
   }
   // value of group lane 0 (DPP row_newbcast:0)
   __device__ static __forceinline__ int32_t first(int32_t v) { return __builtin_amdgcn_update_dpp(0, v, 0x150, 0xf, 0xf, false); }
@@ -59,7 +59,7 @@ struct Grp<64> {
   using Mask = unsigned long long;
   __device__ static __forceinline__ int lane() { return threadIdx.x & 63; }
   __device__ static __forceinline__ int base() { return 0; }
-  __device__ static __forceinline__ Mask ballot(bool p) { return (Mask)__ballot(p); }
+  __device__ static __forceinline__ Mask ballot(bool p) { return (Mask)__builtin_amdgcn_ballot_w64(p); }
   __device__ static __forceinline__ int32_t first(int32_t v) { return __builtin_amdgcn_readlane(v, 0); }
   __device__ static __forceinline__ int32_t at(int32_t v, int32_t l) {
     return __builtin_amdgcn_readlane(v, __builtin_amdgcn_readfirstlane(l));

@@ -286,7 +286,7 @@ struct Window {
     const int l = lane_id();
 #pragma unroll
     for (int j = 0; j < K; j++) {
-      const uint64_t m = __ballot(v[j] == x && 64 * j + l < n);
+      const uint64_t m = __builtin_amdgcn_ballot_w64(v[j] == x && 64 * j + l < n);
       if (m) return 64 * j + (int32_t)__ffsll((unsigned long long)m) - 1;
     }
     return -1;

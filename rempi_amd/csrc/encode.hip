@@ -34,7 +34,7 @@ __global__ void __launch_bounds__(256) k_tile_hist(const int32_t* __restrict__ r
   __syncthreads();
   const uint32_t v = h[threadIdx.x];
   hist[(int64_t)blockIdx.x * kMaxSets + threadIdx.x] = v;
-  const uint64_t nz = __ballot(v != 0);
+  const uint64_t nz = __builtin_amdgcn_ballot_w64(v != 0);
   if (lane_id() == 0 && (uint32_t)nz) atomicOr(&presence[t.rank * (kMaxSets / 32) + wave_id() * 2], (uint32_t)nz);
   if (lane_id() == 32 && (uint32_t)(nz >> 32)) atomicOr(&presence[t.rank * (kMaxSets / 32) + wave_id() * 2 + 1], (uint32_t)(nz >> 32));
 }
@@ -118,10 +118,10 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
     const bool valid = i < t.len;
     const int32_t sid = hi[j].w;
     const int tb = valid ? dense[t.rank * kMaxSets + ((uint32_t)sid < (uint32_t)kMaxSets ? sid : 0)] : 0;
-    uint64_t peers = __ballot(valid);
+    uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
 #pragma unroll
     for (int b = 0; b < 8; b++) {
-      uint64_t m = __ballot((tb >> b) & 1);
+      uint64_t m = __builtin_amdgcn_ballot_w64(((tb >> b) & 1) != 0);
       peers &= ((tb >> b) & 1) ? m : ~m;
     }
     my_t[j] = tb;
@@ -997,7 +997,7 @@ __global__ void __launch_bounds__(256, 8) k_deltas(const Unit* __restrict__ unit
         const uint32_t yt = y & 3;
         const int32_t pt = (int32_t)(y >> 2);
         const bool c = (z < s) & ((yt == kIgn) | ((yt == kRem) & (pt > s)) | ((yt == kAdd) & (pt < s)));
-        d += __popc((uint32_t)(__ballot(c) >> (16 * gw)) & 0xFFFFu);
+        d += __popc((uint32_t)(__builtin_amdgcn_ballot_w64(c) >> (16 * gw)) & 0xFFFFu);
       }
       if (j == 0) items[it].y = (((uint32_t)item.y & 3) == kRem) ? -d : d;
     }
