@@ -447,10 +447,11 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   uint64_t* d_ep_rank = c->buf<uint64_t>("ep_rank", N);
   uint64_t* d_ep_clk = c->buf<uint64_t>("ep_clk", N);
   int32_t* d_segend = c->buf<int32_t>("segend", N);
+  int32_t* d_opn = c->buf<int32_t>("opn", N);  // first untaken column of every row (k_cuts)
   auto epoch_cuts = [&]() {
     c->launch(K_EPOCH, k_epoch<512>, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, d_err);
     // Chain: closed-prefix segments simulated independently, then stitched (chain.hip).
-    c->launch(K_CUTS, k_cuts, dim3(NU), dim3(256), s, d_units, (const int32_t*)d_cord, d_segend);
+    c->launch(K_CUTS, k_cuts, dim3(NU), dim3(256), s, d_units, (const int32_t*)d_inv, d_segend, d_opn);
     c->check_err(d_err, s);
     units = c->download(d_units, NU, s);
   };
@@ -516,7 +517,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     if (c->chain_tier <= 0) {
       c->launch(K_CHAIN_G16, k_chain_grp<16>,
                 dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(c->chain_grid, blocks(n, 64)))), dim3(256), s,
-                (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par, d_exta,
+                (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,
                 d_topg, d_qn, d_ovf1, d_cnt + 1, d_err);
       list = d_ovf1;
       nlist = d_cnt + 1;
@@ -526,7 +527,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     if (c->chain_tier <= 1) {
       const int64_t g64 = c->chain_tier <= 0 ? std::min<int64_t>(1024, blocks(nsegs, 4)) : blocks(n, 4);
       c->launch(K_CHAIN_G64, k_chain_grp<64>, dim3((unsigned)std::max<int64_t>(1, g64)), dim3(256), s,
-                (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par, d_exta,
+                (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,
                 d_topg, d_qn, d_ovf2, d_cnt + 2, d_err);
       list = d_ovf2;
     }
@@ -539,7 +540,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     int2* d_leaves = n > 0 ? c->buf<int2>("leaves", w1n) : nullptr;  // lane tier only
     if (n > 0)
       c->launch(K_CHAIN_SEG, k_chain_seg<16>, dim3((unsigned)std::min<int64_t>(1024, blocks(n, 256))), dim3(256), s,
-                (const Unit*)d_units, d_segs, (int32_t)n, list, (const int32_t*)d_cord, (const int32_t*)d_inv, d_par,
+                (const Unit*)d_units, d_segs, (int32_t)n, list, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par,
                 d_exta, d_topg, d_qn, d_leaves, (const int64_t*)d_w1, d_err,
                 c->chain_stats ? c->buf<unsigned long long>("chain_stats", 8) : (unsigned long long*)nullptr);
     c->chain_tier_counts[2] = n;

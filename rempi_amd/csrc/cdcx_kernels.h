@@ -40,7 +40,7 @@ __global__ void k_rank_tiles(const Unit*, const SortTile*, const uint64_t*, cons
 template <int HCAP>
 __global__ void k_epoch(Unit*, const uint64_t*, uint64_t*, uint64_t*, uint32_t*);
 // chain.hip
-__global__ void k_cuts(Unit*, const int32_t*, int32_t*);
+__global__ void k_cuts(Unit*, const int32_t*, int32_t*, int32_t*);
 __global__ void k_seg_list(const Unit*, const int32_t*, Seg*);
 __global__ void k_seg_hist(const Seg*, int32_t, int32_t*);
 __global__ void k_seg_bins(int32_t*);

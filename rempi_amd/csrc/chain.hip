@@ -30,20 +30,27 @@
 
 namespace cdcx {
 
-// Segment ends: rows r with max(c[0..r]) == r.  One workgroup per unit.
-__global__ void __launch_bounds__(256) k_cuts(Unit* __restrict__ units, const int32_t* __restrict__ cord,
-                                              int32_t* __restrict__ segend) {
+// Segment ends and the first untaken column of every row, one workgroup per unit, in one pass
+// over inv (inv[k] = row that takes column k).  With pm[k] = max(inv[0..k]):
+//  * the prefix of rows 0..k is closed (holds exactly the columns 0..k) iff pm[k] == k -- the
+//    same cuts as max(c[0..r]) == r;
+//  * column k is the first untaken column exactly while the rows processed so far include
+//    pm[k-1] but not pm[k], so opn[i] = k for rows i in (pm[k-1], pm[k]]: the first column not
+//    taken by rows < i, which is what the chain rule compares a new node's column with
+//    (current_column_of_start_it, rempi_clock_delta_compression.cpp:252, :303-316).
+__global__ void __launch_bounds__(256) k_cuts(Unit* __restrict__ units, const int32_t* __restrict__ inv,
+                                              int32_t* __restrict__ segend, int32_t* __restrict__ opn) {
   __shared__ int32_t lds[4];
   Unit& u = units[blockIdx.x];
   if (u.wfail != 0) return;  // not ranked yet (k_window_rank), or already done
   const int64_t a = u.a;
   const int32_t M = u.M;
   int32_t cmax = -1, cn = 0;
-  // 4 rows per thread per round; the next round's columns are loaded during this one
+  // 4 columns per thread per round; the next round's rows are loaded during this one
   int32_t vn[4];
   auto load = [&](int32_t r0) {
 #pragma unroll
-    for (int q = 0; q < 4; q++) vn[q] = (r0 + q < M) ? cord[a + r0 + q] : -1;
+    for (int q = 0; q < 4; q++) vn[q] = (r0 + q < M) ? inv[a + r0 + q] : -1;
   };
   load(4 * threadIdx.x);
   for (int32_t b = 0; b < M; b += 1024) {
@@ -61,7 +68,10 @@ __global__ void __launch_bounds__(256) k_cuts(Unit* __restrict__ units, const in
     int32_t nc = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
+      const int32_t before = run;
       run = max(run, v[q]);
+      if (r0 + q < M)
+        for (int32_t i = before + 1; i <= run; i++) opn[a + i] = r0 + q;
       cut[q] = r0 + q < M && run == r0 + q;
       nc += cut[q] ? 1 : 0;
     }
@@ -174,7 +184,7 @@ struct Stream4 {
 template <int NL>
 __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ units, Seg* __restrict__ segs, int32_t nsegs,
                                                    const int32_t* __restrict__ order, const int32_t* __restrict__ cord,
-                                                   const int32_t* __restrict__ inv, int32_t* __restrict__ par,
+                                                   const int32_t* __restrict__ opn, int32_t* __restrict__ par,
                                                    int32_t* __restrict__ exta, int32_t* __restrict__ topg,
                                                    int32_t* __restrict__ qn, int2* __restrict__ leafg,
                                                    const int64_t* __restrict__ w1, uint32_t* err,
@@ -235,6 +245,7 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
       continue;
     }
     const int32_t c = cs.get(cord, a + i);
+    open = is.get(opn, a + i);  // first column not taken by rows < i (k_cuts)
     if (stats) {
       st_ev++;
       st_slow += slow;
@@ -404,10 +415,6 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
         }
         nl = w;
       }
-    }
-    while (open < s1 && is.get(inv, a + open) <= i) {
-      open++;
-      if (stats) st_open++;
     }
     i++;
   }

@@ -5,7 +5,8 @@
 // but the per-segment state lives *across* the G lanes of a group:
 //   lane j holds leaf slot j (leaves in creation order: id, level, column),
 //   lane j holds the patience top of level lmax - j (the top G levels; lower ones spill),
-//   lane j holds cord/inv of row/column base + j (two G-row windows each, prefetched),
+//   lane j holds cord and opn (first untaken column, k_cuts) of row base + j (two G-row
+//   windows each, prefetched),
 //   lane j buffers par of row cb + j until the window is flushed (coalesced store).
 // Every leaf-list operation of the lane kernel (first qualifying slot, erase, append, sweep)
 // becomes one or two lane-parallel instructions plus a ballot, so an event costs ~70 VALU
@@ -81,7 +82,7 @@ constexpr int ring_rows() { return G == 16 ? 128 : 256; }
 template <int G>
 __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ units, Seg* __restrict__ segs,
                                                    const int32_t* __restrict__ list, const int32_t* __restrict__ nlist_p,
-                                                   const int32_t* __restrict__ cord, const int32_t* __restrict__ inv,
+                                                   const int32_t* __restrict__ cord, const int32_t* __restrict__ opn,
                                                    int32_t* __restrict__ par, int32_t* __restrict__ exta,
                                                    int32_t* __restrict__ topg, int32_t* __restrict__ qn,
                                                    int32_t* __restrict__ ovf, int32_t* __restrict__ novf, uint32_t* err) {
@@ -100,9 +101,9 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
   // group-uniform state
   int32_t si = -1, s0 = 0, s1 = 0, ord = 0;
   int64_t a = 0;
-  int32_t i = 0, open = 0, nl = 0, lmax = 0, nrel1 = 0, qcnt = 0, cb = 0, ob = 0;
+  int32_t i = 0, nl = 0, lmax = 0, nrel1 = 0, qcnt = 0, cb = 0;
   // lane state
-  int32_t lid = 0, llv = 0, lcol = 0, top = 0, cw0 = 0, cw1 = 0, iw0 = 0, iw1 = 0, pval = 0;
+  int32_t lid = 0, llv = 0, lcol = 0, top = 0, cw0 = 0, cw1 = 0, ow0 = 0, ow1 = 0, pval = 0;
 
   auto node = [&](int32_t x) -> int2 {  // {par, column} of row x < i of this segment
     if (x >= i - R) return ring[x & (R - 1)];
@@ -129,12 +130,12 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
       s0 = sg.start;
       s1 = sg.start + sg.len;
       ord = sg.ord;
-      i = open = cb = ob = s0;
+      i = cb = s0;
       nl = lmax = nrel1 = qcnt = 0;
       cw0 = (s0 + j < s1) ? cord[a + s0 + j] : 0;
       cw1 = (s0 + G + j < s1) ? cord[a + s0 + G + j] : 0;
-      iw0 = (s0 + j < s1) ? inv[a + s0 + j] : 0;
-      iw1 = (s0 + G + j < s1) ? inv[a + s0 + G + j] : 0;
+      ow0 = (s0 + j < s1) ? opn[a + s0 + j] : 0;
+      ow1 = (s0 + G + j < s1) ? opn[a + s0 + G + j] : 0;
       // (no `continue`: the first event follows in this iteration; a single loop back-edge
       // keeps the compiler from copying the whole loop state through extra phi blocks)
     } else if (i - cb == G) {  // flush this window's parents, slide the cord window
@@ -142,11 +143,16 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
       cb += G;
       cw0 = cw1;
       cw1 = (cb + G + j < s1) ? cord[a + cb + G + j] : 0;
+      ow0 = ow1;
+      ow1 = (cb + G + j < s1) ? opn[a + cb + G + j] : 0;
     }
     const int32_t t = i - cb;
     // c of row i: lane 0 of the window, which shifts down one lane per row (DPP, no LDS trip)
     const int32_t c = Gr::first(cw0);
     cw0 = Gr::from_next(cw0);
+    // first column not taken by rows < i, likewise
+    const int32_t open = Gr::first(ow0);
+    ow0 = Gr::from_next(ow0);
 
     // ---- k*: highest level whose top column is smaller than c ---------------------------
     const Mask tm = Gr::ballot(j < lmax && top < c);
@@ -261,20 +267,6 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
       }
     }
 
-    // ---- first untaken column ---------------------------------------------------------------
-    while (true) {
-      if (open - ob == G) {
-        ob += G;
-        iw0 = iw1;
-        iw1 = (ob + G + j < s1) ? inv[a + ob + G + j] : 0;
-      }
-      const int32_t to = open - ob;
-      const Mask taken = Gr::ballot(j >= to && ob + j < s1 && iw0 <= i);
-      const Mask run = ~(taken >> to);
-      const int32_t adv = run ? min(Gr::ffs(run), G - to) : G - to;
-      open += adv;
-      if (open - ob < G || open >= s1) break;
-    }
     i++;
   }
 }
