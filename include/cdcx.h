@@ -276,6 +276,18 @@ typedef struct cdcx_replay_stats {
 int cdcx_replay_decode_files(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths,
                              int64_t batch_bytes, cdcx_replay_sink sink, void* user, cdcx_replay_stats* stats);
 
+/* The same pipeline delivering what the reference's replay engine consumes: for every file,
+ * sink(user, i, n_chunks, chunks) receives one cdcx_tables per chunk (in file order) -- the
+ * flat test tables decode() (:1016-1299) would have filled for that chunk, i.e. the inputs of
+ * insert_encoder_input_format_chunk_recv_test_id / cdc_decode_ordering (:1390-1973).  Nothing
+ * is formatted or copied on the host: the arrays point into the context's pinned buffers (the
+ * file image and the packed device output) and are valid only during the call.  The contexts
+ * may live on different devices (one worker thread each sets its context's device).
+ * stats->dump_bytes counts the table descriptors handed over. */
+typedef int (*cdcx_replay_table_sink)(void* user, int32_t file_index, size_t n_chunks, const cdcx_tables* chunks);
+int cdcx_replay_decode_tables(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths,
+                              int64_t batch_bytes, cdcx_replay_table_sink sink, void* user, cdcx_replay_stats* stats);
+
 /* ---------------------------------------------------------------------------------------
  * Synthetic workload (definition in DESIGN.md "Synthetic traces"), generated
  * directly in device memory: n_ranks consecutive ranks starting at first_rank of a job of

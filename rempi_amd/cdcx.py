@@ -72,6 +72,8 @@ class Tables(ctypes.Structure):
 
 _REPLAY_SINK = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.c_int32, _i64p, ctypes.c_size_t)
 
+_REPLAY_TABLE_SINK = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.c_int32, ctypes.c_size_t, P(Tables))
+
 _SIGNATURES = {
     "cdcx_create": ([P(_Opts)], _vp),
     "cdcx_destroy": ([_vp], None),
@@ -97,6 +99,8 @@ _SIGNATURES = {
     "cdcx_verify_roundtrip_device": ([_vp, _vp, _i64p, _vp], ctypes.c_int),
     "cdcx_replay_decode_files": ([P(_vp), ctypes.c_int32, ctypes.c_int32, P(ctypes.c_char_p), ctypes.c_int64,
                                   _REPLAY_SINK, _vp, P(ReplayStats)], ctypes.c_int),
+    "cdcx_replay_decode_tables": ([P(_vp), ctypes.c_int32, ctypes.c_int32, P(ctypes.c_char_p), ctypes.c_int64,
+                                   _REPLAY_TABLE_SINK, _vp, P(ReplayStats)], ctypes.c_int),
     "cdcx_generate_device": ([_vp, P(GenParams), ctypes.c_int32, ctypes.c_int32, P(_vp), _i64p, _vp], ctypes.c_int),
     "cdcx_generate_host": ([P(GenParams), ctypes.c_int32, P(_i32p), P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_set_profiling": ([_vp, ctypes.c_int], ctypes.c_int),
@@ -279,21 +283,7 @@ class Context:
         t = Tables()
         self._check(L.cdcx_decode_chunk(self._c, _ptr(buf, ctypes.c_uint8), len(payload), ctypes.byref(t)), "decode_chunk")
 
-        def arr(ptr, n, dt):
-            return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt).copy() if n else np.zeros(0, dt)
-
-        out = []
-        for i in range(t.n_tables):
-            x = t.tables[i]
-            out.append({"set_id": x.set_id, "count": x.count,
-                        "epoch_rank": arr(x.epoch_rank, x.n_epoch, np.int64),
-                        "epoch_clock": arr(x.epoch_clock, x.n_epoch, np.int64),
-                        "with_previous": arr(x.with_previous, x.n_with_previous, np.int64),
-                        "matched_index": arr(x.matched_index, x.n_matched_index, np.int64),
-                        "unmatched_id": arr(x.unmatched_id, x.n_unmatched, np.int64),
-                        "unmatched_count": arr(x.unmatched_count, x.n_unmatched, np.int64),
-                        "ids": arr(x.ids, x.n_pairs, np.int64), "delays": arr(x.delays, x.n_pairs, np.int64),
-                        "perm": arr(x.perm, x.count, np.int32)})
+        out = [_table_dict(t.tables[i]) for i in range(t.n_tables)]
         L.cdcx_free(t.tables)
         return out
 
@@ -509,6 +499,54 @@ def replay_decode_files(contexts, paths, sink=None, batch_bytes: int = 0) -> dic
     if rc:
         msgs = [L.cdcx_last_error(c._c).decode() for c in contexts]
         raise CdcxError(rc, "replay_decode_files: " + "; ".join(m for m in msgs if m))
+    return {k: getattr(st, k) for k, _ in ReplayStats._fields_}
+
+
+def _table_dict(x: Table) -> dict:
+    def arr(ptr, n, dt):
+        return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt).copy() if n else np.zeros(0, dt)
+
+    return {"set_id": x.set_id, "count": x.count, "epoch_rank": arr(x.epoch_rank, x.n_epoch, np.int64),
+            "epoch_clock": arr(x.epoch_clock, x.n_epoch, np.int64),
+            "with_previous": arr(x.with_previous, x.n_with_previous, np.int64),
+            "matched_index": arr(x.matched_index, x.n_matched_index, np.int64),
+            "unmatched_id": arr(x.unmatched_id, x.n_unmatched, np.int64),
+            "unmatched_count": arr(x.unmatched_count, x.n_unmatched, np.int64),
+            "ids": arr(x.ids, x.n_pairs, np.int64), "delays": arr(x.delays, x.n_pairs, np.int64),
+            "perm": arr(x.perm, x.count, np.int32)}
+
+
+def replay_decode_tables(contexts, paths, sink=None, batch_bytes: int = 0, convert: bool = True) -> dict:
+    """Streaming replay decode delivering flat tables (cdcx_replay_decode_tables).  sink(file_index,
+    chunks) gets, per file, a list (chunks) of lists (tables, ascending set id) of dicts -- copies
+    of the arrays, which only live during the C callback; with convert=False the sink gets
+    (file_index, n_chunks, pointer to cdcx_tables) and must not keep the pointer."""
+    L = lib()
+    ctxs = (_vp * len(contexts))(*[c._c for c in contexts])
+    enc = [os.fsencode(p) for p in paths]
+    arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+    failure = []
+
+    def _sink(_user, i, n_chunks, chunks):
+        if sink is None:
+            return 0
+        try:
+            if not convert:
+                return 1 if sink(int(i), int(n_chunks), chunks) else 0
+            out = [[_table_dict(chunks[k].tables[q]) for q in range(chunks[k].n_tables)] for k in range(n_chunks)]
+            return 1 if sink(int(i), out) else 0
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            failure.append(e)
+            return 1
+
+    cb = _REPLAY_TABLE_SINK(_sink)
+    st = ReplayStats()
+    rc = L.cdcx_replay_decode_tables(ctxs, len(contexts), len(enc), arr, int(batch_bytes), cb, None, ctypes.byref(st))
+    if failure:
+        raise failure[0]
+    if rc:
+        msgs = [L.cdcx_last_error(c._c).decode() for c in contexts]
+        raise CdcxError(rc, "replay_decode_tables: " + "; ".join(m for m in msgs if m))
     return {k: getattr(st, k) for k, _ in ReplayStats._fields_}
 
 

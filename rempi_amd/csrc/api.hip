@@ -1465,7 +1465,8 @@ struct ReplayJob {
   std::atomic<int32_t> next{0};
   std::atomic<bool> stop{false};
   std::mutex sink_mu;
-  cdcx_replay_sink sink;
+  cdcx_replay_sink sink = nullptr;              // int64 dumps, or
+  cdcx_replay_table_sink table_sink = nullptr;  // flat tables pointing into the pinned buffers
   void* user;
   std::atomic<int64_t> chunks{0}, units{0}, records{0}, bytes{0}, dump_bytes{0};
   std::atomic<int64_t> ns_read{0}, ns_device{0}, ns_dump{0}, ns_sink{0};  // thread time per phase
@@ -1531,6 +1532,58 @@ void replay_batch(cdcx_ctx* c, ReplayJob& job, int32_t b, hipStream_t s) {
   job.chunks += (int64_t)c->dchunks.size();
   job.units += (int64_t)c->dunits.size();
   job.records += c->n_rec_out;
+  if (job.table_sink) {
+    // Flat tables of every chunk of every file, nothing copied on the host: epoch lines,
+    // matched_index and unmatched counts are read in place from the file image in the pinned
+    // input buffer, the inverted sections and permutations from the packed D2H buffer.
+    std::vector<cdcx_table> tabs;
+    std::vector<cdcx_tables> chunks;
+    std::map<int32_t, int32_t> bysid;
+    for (int32_t r = 0; r < R; r++) {
+      tabs.clear();
+      chunks.clear();
+      std::vector<size_t> first;
+      for (int32_t k = c->dcbase[r]; k < c->dcbase[r + 1]; k++) {
+        bysid.clear();  // test_tables_map: ascending set id, the last table of an id wins
+        for (int32_t q = 0; q < c->dnunits[k]; q++) bysid[c->dunits[c->dfirst_unit[k] + q].set_id] = c->dfirst_unit[k] + q;
+        first.push_back(tabs.size());
+        for (auto& kv : bysid) {
+          const DUnit& u = c->dunits[kv.second];
+          const uint64_t* wpd = tb.pk + tb.pk_off[kv.second];
+          const size_t U = u.Uc > 0 ? (size_t)u.U : 0;
+          cdcx_table o;
+          o.set_id = u.set_id;
+          o.count = u.M;
+          o.n_epoch = (size_t)u.S;
+          o.epoch_rank = reinterpret_cast<const uint64_t*>(h + u.ep_off);
+          o.epoch_clock = o.epoch_rank + u.S;
+          o.n_with_previous = (size_t)u.W;
+          o.with_previous = wpd;
+          o.n_matched_index = (size_t)u.Mi;
+          o.matched_index = reinterpret_cast<const uint64_t*>(h + u.mi_off);
+          o.n_unmatched = U;
+          o.unmatched_id = wpd + u.W;
+          o.unmatched_count = reinterpret_cast<const uint64_t*>(h + u.ucnt_off);
+          o.n_pairs = (size_t)u.P;
+          o.ids = o.unmatched_id + U;
+          o.delays = o.ids + u.P;
+          o.perm = tb.perm + u.key_off;
+          tabs.push_back(o);
+        }
+      }
+      first.push_back(tabs.size());
+      for (size_t k = 0; k + 1 < first.size(); k++) chunks.push_back(cdcx_tables{first[k + 1] - first[k], tabs.data() + first[k]});
+      job.dump_bytes += (int64_t)(tabs.size() * sizeof(cdcx_table));
+      job.ns_dump += ns_since(t);
+      std::lock_guard<std::mutex> g(job.sink_mu);
+      if (job.stop) return;
+      if (job.table_sink(job.user, f0 + r, chunks.size(), chunks.data()) != 0)
+        throw CdcxError{CDCX_ERR_ARG, "replay sink stopped the pipeline at file " + std::to_string(f0 + r)};
+      job.ns_sink += ns_since(t);
+    }
+    for (int32_t r = 0; r < R; r++) job.bytes += job.size[f0 + r];
+    return;
+  }
   std::vector<int64_t> dump;
   for (int32_t r = 0; r < R; r++) {
     dump.clear();
@@ -1550,9 +1603,34 @@ void replay_batch(cdcx_ctx* c, ReplayJob& job, int32_t b, hipStream_t s) {
 
 extern "C" {
 
+}  // extern "C"
+
+namespace {
+int replay_run(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths, int64_t batch_bytes,
+               cdcx_replay_sink sink, cdcx_replay_table_sink table_sink, void* user, cdcx_replay_stats* stats);
+}
+
+extern "C" {
+
 int cdcx_replay_decode_files(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths,
                              int64_t batch_bytes, cdcx_replay_sink sink, void* user, cdcx_replay_stats* stats) {
-  if (!ctxs || n_ctx <= 0 || n_files < 0 || (n_files && !paths) || !sink) return CDCX_ERR_ARG;
+  if (!sink) return CDCX_ERR_ARG;
+  return replay_run(ctxs, n_ctx, n_files, paths, batch_bytes, sink, nullptr, user, stats);
+}
+
+int cdcx_replay_decode_tables(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths,
+                              int64_t batch_bytes, cdcx_replay_table_sink sink, void* user, cdcx_replay_stats* stats) {
+  if (!sink) return CDCX_ERR_ARG;
+  return replay_run(ctxs, n_ctx, n_files, paths, batch_bytes, nullptr, sink, user, stats);
+}
+
+}  // extern "C"
+
+namespace {
+
+int replay_run(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths, int64_t batch_bytes,
+               cdcx_replay_sink sink, cdcx_replay_table_sink table_sink, void* user, cdcx_replay_stats* stats) {
+  if (!ctxs || n_ctx <= 0 || n_files < 0 || (n_files && !paths)) return CDCX_ERR_ARG;
   for (int32_t i = 0; i < n_ctx; i++) {
     if (!ctxs[i]) return CDCX_ERR_ARG;
     for (int32_t k = 0; k < i; k++)
@@ -1565,6 +1643,7 @@ int cdcx_replay_decode_files(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_fil
   ReplayJob job;
   job.paths = paths;
   job.sink = sink;
+  job.table_sink = table_sink;
   job.user = user;
   job.size.resize(n_files);
   for (int32_t i = 0; i < n_files; i++) {
@@ -1622,6 +1701,10 @@ int cdcx_replay_decode_files(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_fil
     if (rc[w] != CDCX_OK) return rc[w];
   return CDCX_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 int cdcx_generate_host(const cdcx_gen_params* p, int32_t rank, int32_t** rec8, size_t* n_rec) {
   if (!p || !rec8 || !n_rec || p->world_size < 2 || p->events_per_rank < 0) return CDCX_ERR_ARG;

@@ -108,3 +108,49 @@ def test_replay_cli_writes_tables(tmp_path):
     assert replay.main([str(tmp_path / "in"), "--streams", "2", "--out", str(tmp_path / "out")]) == 0
     for r, t in want.items():
         assert (tmp_path / "out" / f"rank_{r}.tables").read_bytes() == t
+
+
+def _as_chunks(dump: bytes):
+    """Reference table dump -> per chunk, per table the fields as comparable python values."""
+    out = []
+    for ch in O.parse_tables(dump):
+        out.append([{k: (t[k].tolist() if hasattr(t[k], "tolist") else t[k]) for k in t} for t in ch])
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("streams,batch_bytes", [(1, 0), (3, 4096)])
+def test_replay_dir_delivers_reference_tables(tmp_path, streams, batch_bytes):
+    """cdcx_replay_decode_tables: the flat tables handed to the sink (pointers into the pinned
+    buffers, no host formatting) hold exactly what the reference decode() leaves in each chunk's
+    test tables."""
+    want = _rempi_dir(tmp_path, n_synth=3)
+    got = {}
+
+    def sink(rank, chunks):
+        got[rank] = chunks
+
+    st, ranks = replay.decode_dir_tables(str(tmp_path), streams=streams, batch_bytes=batch_bytes, sink=sink)
+    assert sorted(got) == sorted(want) == ranks
+    for r in want:
+        ref = _as_chunks(want[r])
+        assert len(got[r]) == len(ref), r
+        for gch, rch in zip(got[r], ref):
+            assert [t["set_id"] for t in gch] == [t["set_id"] for t in rch]
+            for g, w in zip(gch, rch):
+                assert g["count"] == w["count"]
+                for k in ("epoch_rank", "epoch_clock", "with_previous", "matched_index", "ids", "delays", "perm"):
+                    assert g[k].tolist() == w[k], (r, k)
+                um = dict(zip(g["unmatched_id"].tolist(), g["unmatched_count"].tolist()))
+                assert sorted(um.items()) == [tuple(x) for x in w["unmatched"]], r
+    assert st["files"] == len(want)
+
+
+@pytest.mark.gpu
+def test_replay_rejects_a_context_passed_twice(tmp_path):
+    _rempi_dir(tmp_path, n_synth=1)
+    c = cdcx.Context()
+    with pytest.raises(cdcx.CdcxError) as e:
+        cdcx.replay_decode_files([c, c], [p for _, p in replay.rank_files(str(tmp_path))])
+    assert e.value.code == 1
+    c.close()

@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--repeat", type=int, default=2, help="decode passes (the first warms up)")
     ap.add_argument("--keep", action="store_true")
     ap.add_argument("--py-sink", action="store_true", help="hand every dump to a Python sink (bytes copy)")
+    ap.add_argument("--tables", action="store_true",
+                    help="deliver flat tables per chunk (cdcx_replay_decode_tables) instead of int64 dumps")
     a = ap.parse_args()
     ws, rank = int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("RANK", 0))
     dev = int(os.environ.get("LOCAL_RANK", 0))
@@ -67,15 +69,27 @@ def main():
     def sink(r, data):  # a consumer that takes each rank's tables (a bytes copy)
         n_dumped[0] += 1
 
+    n_tables = [0]
+
+    def table_sink(r, n_chunks, chunks):  # a consumer that walks the descriptors it is handed
+        for k in range(n_chunks):
+            n_tables[0] += chunks[k].n_tables
+
     st = None
     for _ in range(max(a.repeat, 1)):
         n_dumped[0] = 0
-        st, _ = replay.decode_dir(d, a.streams, a.batch_mb << 20, 0, dev, sink if a.py_sink else None)
+        n_tables[0] = 0
+        if a.tables:
+            st, _ = replay.decode_dir_tables(d, a.streams, a.batch_mb << 20, 0, dev, table_sink, convert=False)
+        else:
+            st, _ = replay.decode_dir(d, a.streams, a.batch_mb << 20, 0, dev, sink if a.py_sink else None)
     if not a.keep:
         shutil.rmtree(d, ignore_errors=True)
     out = {
         "what": "config 5: streaming replay decode of REMPI_DIR rank files (read -> pinned -> H2D -> decode -> D2H "
-                "tables -> per-rank dumps), page cache warm",
+                "tables -> " + ("flat tables per chunk handed to the sink in place" if a.tables else "per-rank dumps")
+                + "), page cache warm",
+        "mode": "tables" if a.tables else "dumps", "tables_seen": n_tables[0],
         "ranks": hi - lo, "world": a.ranks, "events_per_rank": a.events, "streams": a.streams,
         "records_written": records, "write_s": round(t_write, 2),
         "files": st["files"], "file_gb": round(st["file_bytes"] / 1e9, 3), "records_decoded": st["records"],
