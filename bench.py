@@ -459,6 +459,8 @@ def main():
                   + (f"   alone {so[0] / so[1]:8.3f} ms" if so else ""), file=sys.stderr)
         print(f"  timed {elapsed:.3f}s for {args.steps} steps x {len(plan)} batches on {len(lanes)} streams; "
               f"kernels sum {tot / 1e3:.3f}s; job wall {job_wall:.1f}s", file=sys.stderr)
+        print(f"  chain tiers of the last encode of lane 0 (segments: all, past 16 leaves, past 64): "
+              f"{lanes[0].ctx.chain_tiers()}", file=sys.stderr)
         for note in ver["notes"][:20]:
             print("  verify:", note, file=sys.stderr)
 

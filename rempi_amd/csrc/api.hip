@@ -31,7 +31,7 @@ namespace {
 
 enum KernelId {
   K_SET_PRESENCE, K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_INC0, K_TILE_SUM, K_RANK_SCAN, K_TILE_P0,
-  K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_WINDOW_RANK, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_G16, K_CHAIN_G64, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
+  K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_WINDOW_RANK, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_G8, K_CHAIN_G16, K_CHAIN_G64, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
   K_WRITE_UNITS, K_CHUNK_HEADERS, K_FOOTER_ORDER, K_FOOTER_WRITE, K_WRITE_KEYS,
   K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS, K_DEC_PACK, K_VERIFY,
   K_GEN_TILE_SUMS, K_GEN_RANK_SCAN, K_GEN_FRAMES, K_GEN_AKEYS, K_GEN_ARRIVAL, K_GEN_RECORDS,
@@ -39,7 +39,7 @@ enum KernelId {
 };
 const char* kKernelNames[K_COUNT] = {
   "k_set_presence", "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_inc0", "k_tile_sum", "k_rank_scan",
-  "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_window_rank", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
+  "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_window_rank", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp8", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
   "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records", "k_dec_pack_tables", "k_verify_roundtrip",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
@@ -169,6 +169,7 @@ struct cdcx_ctx {
   int rank_tier = getenv("CDCX_RANK_TIER") ? atoi(getenv("CDCX_RANK_TIER")) : 0;
   // blocks of the 16-lane chain tier (a work queue: fewer blocks leave CUs to other streams)
   int64_t chain_grid = getenv("CDCX_CHAIN_GRID") ? std::max(1, atoi(getenv("CDCX_CHAIN_GRID"))) : 2048;
+  bool chain_g16 = getenv("CDCX_CHAIN_G16") != nullptr;  // first tier on 16-lane groups (A/B timing)
   int64_t chain_tier_counts[3] = {0, 0, 0};  // segments entering each tier in the last encode
 
   template <class T>
@@ -515,10 +516,16 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     const int32_t* nlist = d_cnt;
     int64_t n = nsegs;
     if (c->chain_tier <= 0) {
-      c->launch(K_CHAIN_G16, k_chain_grp<16>,
-                dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(c->chain_grid, blocks(n, 64)))), dim3(256), s,
-                (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,
-                d_topg, d_qn, d_ovf1, d_cnt + 1, d_err);
+      if (c->chain_g16)
+        c->launch(K_CHAIN_G16, k_chain_grp<16>,
+                  dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(c->chain_grid, blocks(n, 64)))), dim3(256), s,
+                  (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,
+                  d_topg, d_qn, d_ovf1, d_cnt + 1, d_err);
+      else
+        c->launch(K_CHAIN_G8, k_chain_grp8,
+                  dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(c->chain_grid, blocks(n, 128)))), dim3(256), s,
+                  (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,
+                  d_topg, d_qn, d_ovf1, d_cnt + 1, d_err);
       list = d_ovf1;
       nlist = d_cnt + 1;
     }

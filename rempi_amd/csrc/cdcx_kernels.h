@@ -51,6 +51,9 @@ __global__ void k_chain_seg(const Unit*, Seg*, int32_t, const int32_t*, const in
 template <int G>
 __global__ void k_chain_grp(const Unit*, Seg*, const int32_t*, const int32_t*, const int32_t*, const int32_t*, int32_t*,
                             int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*);
+// chain_group8.hip
+__global__ void k_chain_grp8(const Unit*, Seg*, const int32_t*, const int32_t*, const int32_t*, const int32_t*, int32_t*,
+                             int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*);
 __global__ void k_chain_exits(const Unit*, const Seg*, int32_t, const int32_t*, const int32_t*, const int32_t*, int32_t*,
                               uint32_t*);
 __global__ void k_chain_entries(Unit*, int32_t, Seg*, const int32_t*);

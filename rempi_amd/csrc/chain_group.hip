@@ -244,6 +244,18 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
       lcol = drop ? ncol : lcol;
       nl -= (pslot >= 0) ? 1 : 0;
     }
+    // (the sweep comes before the append: the new node, on column `open` itself, is never
+    // swept, and a list that is full only until the sweep need not leave the tier)
+    if (c == open) {
+      const Mask dead = Gr::ballot(j < nl && lcol < open);
+      if (dead) {
+        const int32_t dst = (j < nl && !Gr::bit(dead, j)) ? j - Gr::popc(dead & Gr::below(j)) : G - 1;
+        lid = Gr::push(lid, dst);
+        llv = Gr::push(llv, dst);
+        lcol = Gr::push(lcol, dst);
+        nl -= Gr::popc(dead);
+      }
+    }
     if (nl == G) {  // leaf list outgrows the group: hand the segment to the next tier
       if (j == 0) ovf[atomicAdd(novf, 1)] = si;
       si = -1;
@@ -256,16 +268,6 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
       lcol = c;
     }
     nl++;
-    if (c == open) {
-      const Mask dead = Gr::ballot(j < nl && lcol < open);
-      if (dead) {
-        const int32_t dst = (j < nl && !Gr::bit(dead, j)) ? j - Gr::popc(dead & Gr::below(j)) : G - 1;
-        lid = Gr::push(lid, dst);
-        llv = Gr::push(llv, dst);
-        lcol = Gr::push(lcol, dst);
-        nl -= Gr::popc(dead);
-      }
-    }
 
     i++;
   }
