@@ -539,6 +539,7 @@ def algorithmic_bytes(kernel, n_records, c):
         "k_sort_tiles": m * (8 + 8 + 4),
         "k_rank_tiles": m * (8 + 4 + 8 + 4 + 4 + 8),
         "k_epoch": m * 8,
+        "k_chain_grp8": m * (4 + 4 + 4),
         "k_chain_grp16": m * (4 + 4 + 4),
         "k_chain_grp64": m * (4 + 4 + 4),
         "k_chain_mark": m * (4 + 1),

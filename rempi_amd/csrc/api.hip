@@ -516,7 +516,8 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     const int32_t* nlist = d_cnt;
     int64_t n = nsegs;
     if (c->chain_tier <= 0) {
-      if (c->chain_g16)
+      // (the 8-lane kernel addresses rows by 32-bit byte offsets)
+      if (c->chain_g16 || N >= (int64_t(1) << 30))
         c->launch(K_CHAIN_G16, k_chain_grp<16>,
                   dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(c->chain_grid, blocks(n, 64)))), dim3(256), s,
                   (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,

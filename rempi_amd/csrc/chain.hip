@@ -30,14 +30,16 @@
 
 namespace cdcx {
 
-// Segment ends and the first untaken column of every row, one workgroup per unit, in one pass
-// over inv (inv[k] = row that takes column k).  With pm[k] = max(inv[0..k]):
+// Segment ends and the "open" flag of every row, one workgroup per unit, in one pass over inv
+// (inv[k] = row that takes column k).  With pm[k] = max(inv[0..k]):
 //  * the prefix of rows 0..k is closed (holds exactly the columns 0..k) iff pm[k] == k -- the
 //    same cuts as max(c[0..r]) == r;
-//  * column k is the first untaken column exactly while the rows processed so far include
-//    pm[k-1] but not pm[k], so opn[i] = k for rows i in (pm[k-1], pm[k]]: the first column not
-//    taken by rows < i, which is what the chain rule compares a new node's column with
-//    (current_column_of_start_it, rempi_clock_delta_compression.cpp:252, :303-316).
+//  * row i = inv[k] sits on the first column not taken by rows < i exactly when every smaller
+//    column belongs to an earlier row, inv[k] > pm[k-1]: that is what the chain rule tests when
+//    it compares a new node's column with current_column_of_start_it
+//    (rempi_clock_delta_compression.cpp:252, :303-316).
+// opn[i] = column of row i, with bit 31 set when the row is open: the one word per row the
+// chain kernels stream.
 __global__ void __launch_bounds__(256) k_cuts(Unit* __restrict__ units, const int32_t* __restrict__ inv,
                                               int32_t* __restrict__ segend, int32_t* __restrict__ opn) {
   __shared__ int32_t lds[4];
@@ -68,10 +70,8 @@ __global__ void __launch_bounds__(256) k_cuts(Unit* __restrict__ units, const in
     int32_t nc = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const int32_t before = run;
+      if (r0 + q < M) opn[a + v[q]] = (r0 + q) | (v[q] > run ? INT32_MIN : 0);
       run = max(run, v[q]);
-      if (r0 + q < M)
-        for (int32_t i = before + 1; i <= run; i++) opn[a + i] = r0 + q;
       cut[q] = r0 + q < M && run == r0 + q;
       nc += cut[q] ? 1 : 0;
     }
@@ -245,7 +245,7 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
       continue;
     }
     const int32_t c = cs.get(cord, a + i);
-    open = is.get(opn, a + i);  // first column not taken by rows < i (k_cuts)
+    open = is.get(opn, a + i) < 0 ? c : -1;  // c when it is the first column not taken by rows < i (k_cuts)
     if (stats) {
       st_ev++;
       st_slow += slow;

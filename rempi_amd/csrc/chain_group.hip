@@ -151,7 +151,7 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
     const int32_t c = Gr::first(cw0);
     cw0 = Gr::from_next(cw0);
     // first column not taken by rows < i, likewise
-    const int32_t open = Gr::first(ow0);
+    const int32_t open = Gr::first(ow0) < 0 ? c : -1;  // c when row i is open (k_cuts)
     ow0 = Gr::from_next(ow0);
 
     // ---- k*: highest level whose top column is smaller than c ---------------------------

@@ -11,6 +11,18 @@
 // segs[].lmax/qcount) and the same hand-over to the next tier when a list outgrows its 16
 // slots as k_chain_grp<16>.
 //
+// What keeps the instruction count down:
+//  * one word per row: the column with the "open" flag in bit 31 (k_cuts), streamed through a
+//    two-register window per lane that shifts down one lane per row (DPP);
+//  * the eight groups of a wave slide their windows in the same iteration: a segment that
+//    starts at wave phase t puts its first row at window slot t, so the flush of the parent
+//    buffer and the window loads sit behind a scalar branch taken every eighth iteration;
+//  * 32-bit byte offsets from the (scalar) array bases for every global access -- the host
+//    launches this kernel only when the batch has fewer than 2^30 rows;
+//  * group ballots as scalar compare masks (no select/compare round trip per ballot);
+//  * ancestor climbs read the LDS ring directly; the global fallback for rows older than the
+//    ring sits behind a branch.
+//
 // 8-lane groups on 16-lane DPP rows: a row shift leaks one value of the neighbouring group
 // into lane 7 (row_shl) or lane 0 (row_shr) of a group; every use below either overwrites
 // that lane or leaves it outside the live part of the list / window.  Broadcasts of a group's
@@ -24,27 +36,35 @@ namespace cdcx {
 
 namespace {
 constexpr int G8 = 8;
-constexpr int kRing8 = 64;  // rows of {par, column} per group in LDS
+constexpr int kRing8 = 64;      // rows of {par, column} per group in LDS
 constexpr int kLongSeg = 1536;  // events: segments from here on run at raised wave priority
 
-__device__ __forceinline__ int lane8() { return threadIdx.x & 7; }
-__device__ __forceinline__ int base8() { return threadIdx.x & 56; }
-__device__ __forceinline__ uint32_t ballot8(bool p) {
-  return (uint32_t)((unsigned long long)__builtin_amdgcn_ballot_w64(p) >> base8()) & 0xFFu;
-}
+using mask64 = unsigned long long;
+// lane masks of a signed compare, straight from v_cmp (LLVM integer predicates)
+__device__ __forceinline__ mask64 m_lt(int32_t x, int32_t y) { return __builtin_amdgcn_sicmp(x, y, 40); }
+__device__ __forceinline__ mask64 m_gt(int32_t x, int32_t y) { return __builtin_amdgcn_sicmp(x, y, 38); }
+__device__ __forceinline__ mask64 m_eq(int32_t x, int32_t y) { return __builtin_amdgcn_sicmp(x, y, 32); }
+// the group's byte of a lane mask (sh = the group's first lane)
+__device__ __forceinline__ uint32_t grp8(mask64 m, int sh) { return (uint32_t)(m >> sh) & 0xFFu; }
+
 // value of the group's lane 0
 __device__ __forceinline__ int32_t first8(int32_t v) {
   int32_t t = __builtin_amdgcn_update_dpp(0, v, 0x150, 0xf, 0x3, false);  // row_newbcast:0 -> lanes 0-7 of the row
   return __builtin_amdgcn_update_dpp(t, v, 0x158, 0xf, 0xC, false);       // row_newbcast:8 -> lanes 8-15
 }
-// value of group lane l (l group-uniform)
-__device__ __forceinline__ int32_t at8(int32_t v, int32_t l) { return __builtin_amdgcn_ds_bpermute((base8() + l) << 2, v); }
 // lane j <- lane j+1 (the group's lane 7 receives the neighbouring group's lane 0, or keeps its value)
 __device__ __forceinline__ int32_t next8(int32_t v) { return __builtin_amdgcn_update_dpp(v, v, 0x101, 0xf, 0xf, false); }
 // lane j <- lane j-1 (the group's lane 0 receives the neighbouring group's lane 7, or keeps its value)
 __device__ __forceinline__ int32_t prev8(int32_t v) { return __builtin_amdgcn_update_dpp(v, v, 0x111, 0xf, 0xf, false); }
-__device__ __forceinline__ int32_t push8(int32_t v, int32_t dst) { return __builtin_amdgcn_ds_permute((base8() + dst) << 2, v); }
 __device__ __forceinline__ uint32_t below(int j) { return (1u << j) - 1u; }
+
+// global accesses at a 32-bit byte offset from a wave-uniform base
+__device__ __forceinline__ int32_t ldg(const int32_t* base, uint32_t boff) {
+  return *reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(base) + boff);
+}
+__device__ __forceinline__ void stg(int32_t* base, uint32_t boff, int32_t v) {
+  *reinterpret_cast<int32_t*>(reinterpret_cast<char*>(base) + boff) = v;
+}
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ units, Seg* __restrict__ segs,
@@ -57,33 +77,60 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
   constexpr int kGroups = 256 / G;
   constexpr int R = kRing8;
   __shared__ int32_t next_j;
-  __shared__ int2 ring_all[kGroups][R];   // {par, column} of row r at [r % R]
+  __shared__ int2 ring_all[kGroups][R];          // {par, column} of row r at [r % R]
   __shared__ int32_t comp_all[kGroups][3 * 16];  // sweep compaction of a list that uses the B slots
   int2* ring = ring_all[threadIdx.x / G];
   int32_t* comp = comp_all[threadIdx.x / G];
   if (threadIdx.x == 0) next_j = 0;
   __syncthreads();
 
-  const int j = lane8();
+  const int j = threadIdx.x & 7;
+  const int sh = threadIdx.x & 56;     // the group's first lane in the wave
+  const int32_t bp4 = sh << 2;         // its ds_bpermute / ds_permute address
   const int32_t nlist = *nlist_p;
-  // group-uniform state
+  // group-uniform state.  ab / tb: byte offsets of the unit's row 0 / the segment's row 0.
   int32_t si = -1, s0 = 0, s1 = 0, ord = 0;
-  int64_t a = 0;
-  int32_t i = 0, nl = 0, lmax = 0, nrel1 = 0, qcnt = 0, cb = 0;
+  uint32_t ab = 0, tb = 0;
+  int32_t i = 0, nl = 0, lmax = 0, nrel1 = 0, qcnt = 0;
   bool islong = false;
-  // lane state: leaf slots j (A) and 8 + j (B), top of level lmax - j, row windows, parent buffer
+  // lane state: leaf slots j (A) and 8 + j (B), top of level lmax - j, the row window (row
+  // i + j in cw0 while it lies in the current eight-row frame, the next frame in cw1), the
+  // frame's parents (row rj = frame start + j)
   int32_t lid = 0, llv = 0, lcol = 0, lidB = 0, llvB = 0, lcolB = 0;
-  int32_t top = 0, cw0 = 0, cw1 = 0, ow0 = 0, ow1 = 0, pval = 0;
+  int32_t top = 0, cw0 = 0, cw1 = 0, pval = 0, rj = j;
+  // wave-uniform phase: every group's row i sits at slot t of its frame
+  int t = 0;
 
-  auto node = [&](int32_t x) -> int2 {  // {par, column} of row x < i of this segment
-    if (x >= i - R) return ring[x & (R - 1)];
-    return make_int2(par[a + x], cord[a + x]);
+  auto ring_par = [&](int32_t x) -> int32_t {  // parent of row x < i of this segment
+    int32_t p = ring[x & (R - 1)].x;
+    asm volatile("" : "+v"(p));  // keeps the LDS read an LDS read (no flat load of a selected address)
+    if (x < i - R) p = ldg(par, ab + 4u * (uint32_t)x);
+    return p;
+  };
+  auto ring_col = [&](int32_t x) -> int32_t {
+    int32_t q = ring[x & (R - 1)].y;
+    asm volatile("" : "+v"(q));
+    if (x < i - R) q = ldg(cord, ab + 4u * (uint32_t)x);
+    return q;
   };
 
   while (true) {
+    if (t == G) {  // every group at once: store the frame's parents, slide the windows
+      t = 0;
+      if (rj >= s0) stg(par, ab + 4u * (uint32_t)rj, pval);  // (rows before s0: the previous segment's, stored there)
+      rj += G;
+      cw0 = cw1;
+      cw1 = (rj + G < s1) ? ldg(opn, ab + 4u * (uint32_t)rj + 4u * G) : 0;
+      // The kernel ends when its longest segments end, and they share their SIMD with other
+      // waves all the way: a wave that runs one of them issues ahead of the others.
+      if (__builtin_amdgcn_ballot_w64(islong) != 0)
+        __builtin_amdgcn_s_setprio(3);
+      else
+        __builtin_amdgcn_s_setprio(0);
+    }
     if (i >= s1) {
       if (si >= 0) {
-        if (cb + j < s1) par[a + cb + j] = pval;
+        if (j < t && rj >= s0) stg(par, ab + 4u * (uint32_t)rj, pval);
         if (j == 0) {
           segs[si].lmax = lmax;
           segs[si].qcount = qcnt;
@@ -96,49 +143,32 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
       if (kk >= nlist) break;
       si = list[kk];
       const Seg sg = segs[si];
-      a = units[sg.unit].a;
+      ab = (uint32_t)units[sg.unit].a << 2;
       s0 = sg.start;
       s1 = sg.start + sg.len;
       ord = sg.ord;
-      i = cb = s0;
+      tb = ab + 4u * (uint32_t)s0;
+      i = s0;
+      rj = s0 - t + j;
       nl = lmax = nrel1 = qcnt = 0;
-      // The kernel ends when its longest segments end, and they share their SIMD with other
-      // waves all the way: a wave that runs one of them issues ahead of the others.
       islong = sg.len >= kLongSeg;
-      if (__builtin_amdgcn_ballot_w64(islong) != 0)
-        __builtin_amdgcn_s_setprio(3);
-      else
-        __builtin_amdgcn_s_setprio(0);
-      cw0 = (s0 + j < s1) ? cord[a + s0 + j] : 0;
-      cw1 = (s0 + G + j < s1) ? cord[a + s0 + G + j] : 0;
-      ow0 = (s0 + j < s1) ? opn[a + s0 + j] : 0;
-      ow1 = (s0 + G + j < s1) ? opn[a + s0 + G + j] : 0;
-    } else if (i - cb == G) {  // flush this window's parents, slide the row windows
-      par[a + cb + j] = pval;
-      cb += G;
-      cw0 = cw1;
-      cw1 = (cb + G + j < s1) ? cord[a + cb + G + j] : 0;
-      ow0 = ow1;
-      ow1 = (cb + G + j < s1) ? opn[a + cb + G + j] : 0;
+      cw0 = (j < G - t && s0 + j < s1) ? ldg(opn, tb + 4u * j) : 0;
+      cw1 = (rj + G < s1) ? ldg(opn, ab + 4u * (uint32_t)(rj + G)) : 0;
     }
-    const int32_t t = i - cb;
-    const int32_t c = first8(cw0);     // column of row i
+    const int32_t cv = first8(cw0);  // row i: column, bit 31 = first column not taken by rows < i
     cw0 = next8(cw0);
-    const int32_t open = first8(ow0);  // first column not taken by rows < i
-    ow0 = next8(ow0);
+    const int32_t c = cv & 0x7fffffff;
     // does any group of this wave use its B slots in this iteration?
-    const bool useB = __builtin_amdgcn_ballot_w64(nl > G) != 0;
+    const bool useB = m_gt(nl, G) != 0;
 
     // ---- k*: highest level whose top column is smaller than c ---------------------------
-    const uint32_t tm = ballot8(j < lmax && top < c);
-    int32_t ks = 0;
-    if (tm) {
-      ks = lmax - (__ffs(tm) - 1);
-    } else if (lmax > G) {  // below the register tops: binary search the spilled levels
+    const uint32_t tm = grp8(m_lt(j, lmax) & m_lt(top, c), sh);
+    int32_t ks = tm ? lmax - (__ffs(tm) - 1) : 0;
+    if (tm == 0 && lmax > G) {  // below the register tops: binary search the spilled levels
       int32_t lo = 1, hi = lmax - G;
       while (lo <= hi) {
         const int32_t mid = (lo + hi) >> 1;
-        if (topg[a + s0 + mid - 1] < c) {
+        if (ldg(topg, tb + 4u * (uint32_t)mid - 4u) < c) {
           ks = mid;
           lo = mid + 1;
         } else {
@@ -148,17 +178,19 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
     }
 
     // ---- parent --------------------------------------------------------------------------
-    int32_t pv, pslot = -1;
+    int32_t pv, pslot = 2 * G;  // pslot: the adopted leaf's slot, 16 = none
     if (ks >= 1) {
-      uint32_t eq = ballot8(j < nl && llv == ks && lcol < c);
-      uint32_t gt = ballot8(j < nl && llv > ks);
+      const mask64 jn = m_lt(j, nl);
+      uint32_t eq = grp8(jn & m_eq(llv, ks) & m_lt(lcol, c), sh);
+      uint32_t gt = grp8(jn & m_gt(llv, ks), sh);
       if (useB) {
-        eq |= ballot8(j + G < nl && llvB == ks && lcolB < c) << G;
-        gt |= ballot8(j + G < nl && llvB > ks) << G;
+        const mask64 jnB = m_lt(j + G, nl);
+        eq |= grp8(jnB & m_eq(llvB, ks) & m_lt(lcolB, c), sh) << G;
+        gt |= grp8(jnB & m_gt(llvB, ks), sh) << G;
       }
-      const int wa = eq ? __ffs(eq) - 1 : 2 * G;
+      const uint32_t wa = __builtin_ctz(eq | (1u << (2 * G)));  // first eligible level-k* leaf, 16 = none
       const uint32_t need = gt & below(wa);
-      int win = wa;
+      uint32_t win = wa;
       int32_t anc = -1;
       bool interior = false;
       if (need) {
@@ -166,25 +198,31 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
         const bool mine = (need >> j) & 1u;
         int32_t x = lid, col = 0x7fffffff;
         if (mine) {
-          for (int32_t d = llv - ks; d > 0; d--) x = node(x).x;
-          col = node(x).y;
+#pragma unroll 1
+          for (int32_t d = llv - ks; d > 0; d--) x = ring_par(x);
+          col = ring_col(x);
         }
-        uint32_t ok = ballot8(mine && col < c);
+        uint32_t ok = grp8(m_lt(col, c), sh);
         int32_t xB = lidB;
         if (useB) {
           const bool mineB = (need >> (j + G)) & 1u;
           int32_t colB = 0x7fffffff;
           if (mineB) {
-            for (int32_t d = llvB - ks; d > 0; d--) xB = node(xB).x;
-            colB = node(xB).y;
+#pragma unroll 1
+            for (int32_t d = llvB - ks; d > 0; d--) xB = ring_par(xB);
+            colB = ring_col(xB);
           }
-          ok |= ballot8(mineB && colB < c) << G;
+          ok |= grp8(m_lt(colB, c), sh) << G;
         }
         if (ok) {
           win = __ffs(ok) - 1;
           interior = true;
-          const int32_t aA = at8(x, win & 7), aB = at8(xB, win & 7);
-          anc = win < G ? aA : aB;
+          const int32_t ad = bp4 + ((win & 7) << 2);
+          anc = __builtin_amdgcn_ds_bpermute(ad, x);
+          if (useB) {
+            const int32_t aB = __builtin_amdgcn_ds_bpermute(ad, xB);
+            anc = win < G ? anc : aB;
+          }
         }
       }
       if (win >= 2 * G) {
@@ -194,11 +232,11 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
       if (interior) {
         pv = anc;
       } else {
-        const int32_t pA = at8(lid, win & 7);
-        pv = pA;
+        const int32_t ad = bp4 + ((win & 7) << 2);
+        pv = __builtin_amdgcn_ds_bpermute(ad, lid);
         if (useB) {
-          const int32_t pB = at8(lidB, win & 7);
-          pv = win < G ? pA : pB;
+          const int32_t pB = __builtin_amdgcn_ds_bpermute(ad, lidB);
+          pv = win < G ? pv : pB;
         }
         pslot = win;
       }
@@ -208,22 +246,22 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
       // outside parent, resolved at stitching from (ordinal, first leaf) -- chain.hip
       pv = -2 - nrel1;
       const int32_t f = first8(lid);
-      if (j == 0) exta[a + i] = nl > 0 ? f : -1;
+      if (j == 0) stg(exta, ab + 4u * (uint32_t)i, nl > 0 ? f : -1);
       nrel1++;
     }
-    if (j == t) pval = pv;
+    pval = (j == t) ? pv : pval;
     if (j == 0) ring[i & (R - 1)] = make_int2(pv, c);
 
     // ---- tops ------------------------------------------------------------------------------
     const int32_t k = ks + 1;
     const bool grow = k > lmax;
-    if (grow && j == G - 1 && lmax - (G - 1) >= 1) topg[a + s0 + (lmax - (G - 1)) - 1] = top;
-    if (!grow && lmax - k >= G && j == 0) topg[a + s0 + k - 1] = c;
+    if (grow && j == G - 1 && lmax >= G) stg(topg, tb + 4u * (uint32_t)lmax - 4u * G, top);
+    if (!grow && lmax - k >= G && j == 0) stg(topg, tb + 4u * (uint32_t)k - 4u, c);
     const int32_t tshift = prev8(top);
     top = grow ? ((j == 0) ? c : tshift) : ((j == lmax - k) ? c : top);
     qcnt = grow ? 0 : qcnt;
     lmax = grow ? k : lmax;
-    if (k == lmax && j == 0) qn[a + s0 + qcnt] = i;
+    if (k == lmax && j == 0) stg(qn, tb + 4u * (uint32_t)qcnt, i);
     qcnt += (k == lmax) ? 1 : 0;
 
     // ---- leaves: drop the adopted one, sweep, append the new node --------------------------
@@ -238,30 +276,32 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
           ncol = bcol;
         }
         const int32_t nidB = next8(lidB), nlvB = next8(llvB), ncolB = next8(lcolB);
-        const bool dropB = pslot >= 0 && j + G >= pslot;
+        const bool dropB = j + G >= (int32_t)pslot;
         lidB = dropB ? nidB : lidB;
         llvB = dropB ? nlvB : llvB;
         lcolB = dropB ? ncolB : lcolB;
       }
-      const bool drop = pslot >= 0 && j >= pslot;
+      const bool drop = j >= (int32_t)pslot;
       lid = drop ? nid : lid;
       llv = drop ? nlv : llv;
       lcol = drop ? ncol : lcol;
-      nl -= (pslot >= 0) ? 1 : 0;
+      nl -= (pslot < 2 * G) ? 1 : 0;
     }
-    // (the sweep comes before the append: the new node, on column `open` itself, is never swept)
-    if (c == open) {
-      uint32_t dead = ballot8(j < nl && lcol < open);
+    // (the sweep comes before the append: the new node, on the open column itself, is never swept)
+    if (cv < 0) {
+      uint32_t dead = grp8(m_lt(j, nl) & m_lt(lcol, c), sh);
       if (!useB) {
         if (dead) {
-          const int32_t dst = (j < nl && !((dead >> j) & 1u)) ? j - __popc(dead & below(j)) : G - 1;
-          lid = push8(lid, dst);
-          llv = push8(llv, dst);
-          lcol = push8(lcol, dst);
+          const bool alive = j < nl && !((dead >> j) & 1u);
+          const int32_t dst = alive ? j - __popc(dead & below(j)) : G - 1;
+          const int32_t ad = bp4 + (dst << 2);
+          lid = __builtin_amdgcn_ds_permute(ad, lid);
+          llv = __builtin_amdgcn_ds_permute(ad, llv);
+          lcol = __builtin_amdgcn_ds_permute(ad, lcol);
           nl -= __popc(dead);
         }
       } else {
-        dead |= ballot8(j + G < nl && lcolB < open) << G;
+        dead |= grp8(m_lt(j + G, nl) & m_lt(lcolB, c), sh) << G;
         if (dead) {
           // compaction through LDS: slot s (alive) lands at s - #dead below it
           const bool aliveA = j < nl && !((dead >> j) & 1u), aliveB = j + G < nl && !((dead >> (j + G)) & 1u);
@@ -289,25 +329,33 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
         }
       }
     }
-    if (nl == 2 * G) {  // leaf list outgrows the group: hand the segment to the next tier
-      if (j == 0) ovf[atomicAdd(novf, 1)] = si;
-      si = -1;
-      i = s1 - 1;  // the rest of this iteration runs on junk state and ends the segment
-      nl = 0;
+    if (useB) {
+      if (nl == 2 * G) {  // leaf list outgrows the group: hand the segment to the next tier
+        if (j == 0) ovf[atomicAdd(novf, 1)] = si;
+        si = -1;
+        s1 = i + 1;  // the rest of this iteration runs on junk state and ends the segment
+        nl = 0;
+      }
+      if (j + G == nl) {
+        lidB = i;
+        llvB = k;
+        lcolB = c;
+      }
+    } else if (m_eq(nl, G) != 0) {  // a list filling its eighth slot appends to B slot 0
+      if (j + G == nl) {
+        lidB = i;
+        llvB = k;
+        lcolB = c;
+      }
     }
     if (j == nl) {
       lid = i;
       llv = k;
       lcol = c;
     }
-    if (j + G == nl) {
-      lidB = i;
-      llvB = k;
-      lcolB = c;
-    }
     nl++;
-
     i++;
+    t++;
   }
 }
 
