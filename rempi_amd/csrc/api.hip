@@ -31,7 +31,7 @@ namespace {
 
 enum KernelId {
   K_SET_PRESENCE, K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_INC0, K_TILE_SUM, K_RANK_SCAN, K_TILE_P0,
-  K_CHUNKS, K_UNITS_LB, K_UNIT_PREP, K_WINDOW_RANK, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_G8, K_CHAIN_G16, K_CHAIN_G64, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
+  K_CHUNKS, K_UNITS_LB, K_LISTS, K_UNIT_PREP, K_WINDOW_RANK, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_G8, K_CHAIN_G16, K_CHAIN_G64, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
   K_WRITE_UNITS, K_CHUNK_HEADERS, K_FOOTER_ORDER, K_FOOTER_WRITE, K_WRITE_KEYS,
   K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS, K_DEC_PACK, K_VERIFY,
   K_GEN_TILE_SUMS, K_GEN_RANK_SCAN, K_GEN_FRAMES, K_GEN_AKEYS, K_GEN_ARRIVAL, K_GEN_RECORDS,
@@ -39,7 +39,7 @@ enum KernelId {
 };
 const char* kKernelNames[K_COUNT] = {
   "k_set_presence", "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_inc0", "k_tile_sum", "k_rank_scan",
-  "k_tile_p0", "k_chunks", "k_units_lb", "k_unit_prep", "k_window_rank", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp8", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
+  "k_tile_p0", "k_chunks", "k_units_lb", "k_lists", "k_unit_prep", "k_window_rank", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp8", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
   "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records", "k_dec_pack_tables", "k_verify_roundtrip",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
@@ -142,18 +142,30 @@ struct cdcx_ctx {
     size_t cap = 0;
   };
   Pinned pin_in, pin_tab;  // replay pipeline: rank files in; packed decoded tables out
+  Pinned pin_mail;         // small read-backs between kernels (Mail)
 
   // results of the last encode
   uint8_t* d_out = nullptr;
   int2* d_keys = nullptr;
   int64_t n_keys = 0;
-  std::vector<Unit> enc_units;       // units of the last encode (file order)
+  std::vector<Unit> enc_units;       // units of the last encode (file order); see host_enc_units
+  Unit* d_enc_units = nullptr;       // ... on the device
+  int32_t n_enc_units = 0;
+  bool enc_units_stale = false;      // enc_units not downloaded yet
   std::vector<int64_t> enc_rec_off;  // record offsets of its ranks
   // results of the last decode
   std::vector<DUnit> dunits;
   std::vector<DChunk> dchunks;
   std::vector<int32_t> dfirst_unit, dnunits;
   std::vector<int32_t> dcbase;  // first chunk of each rank file of the last decode (R + 1)
+  // ... the same tables on the device; the host copies above are fetched on demand (host_dec_units)
+  DUnit* d_dunits = nullptr;
+  DChunk* d_dchunks = nullptr;
+  int32_t* d_dnunits = nullptr;
+  int32_t* d_dfirst_unit = nullptr;
+  int32_t n_dunits = 0, n_dchunks = 0;
+  bool dec_host_stale = false;
+  hipStream_t dec_stream = nullptr;  // stream of the last decode
   int32_t* d_rec_out = nullptr;
   int64_t n_rec_out = 0;
   int32_t* d_perm = nullptr;
@@ -255,18 +267,21 @@ struct cdcx_ctx {
     uint32_t e = 0;
     HIPCHK(hipMemcpyAsync(&e, d_err, 4, hipMemcpyDeviceToHost, s));
     collect(s);
-    if (e) {
-      for (int code : {CDCX_ERR_TRUNCATED_EPOCH, CDCX_ERR_CLOCK_ORDER, CDCX_ERR_LIMIT, CDCX_ERR_CORRUPT}) {
-        if (e & (1u << code)) {
-          const char* what = code == CDCX_ERR_TRUNCATED_EPOCH ? "The events in this epoch are truncated"
-                             : code == CDCX_ERR_CLOCK_ORDER   ? "Later message has smaller clock than earlier message"
-                             : code == CDCX_ERR_LIMIT         ? "implementation limit exceeded (set id range or sources per table)"
-                                                              : "Record data is broken";
-          throw CdcxError{code, what};
-        }
+    raise_device_error(e);
+  }
+  // The batch error word (bit = CDCX_ERR_* code) as an exception; 0 = no error.
+  static void raise_device_error(uint32_t e) {
+    if (!e) return;
+    for (int code : {CDCX_ERR_TRUNCATED_EPOCH, CDCX_ERR_CLOCK_ORDER, CDCX_ERR_LIMIT, CDCX_ERR_CORRUPT}) {
+      if (e & (1u << code)) {
+        const char* what = code == CDCX_ERR_TRUNCATED_EPOCH ? "The events in this epoch are truncated"
+                           : code == CDCX_ERR_CLOCK_ORDER   ? "Later message has smaller clock than earlier message"
+                           : code == CDCX_ERR_LIMIT         ? "implementation limit exceeded (set id range or sources per table)"
+                                                            : "Record data is broken";
+        throw CdcxError{code, what};
       }
-      throw CdcxError{CDCX_ERR_CORRUPT, "device error word " + std::to_string(e)};
     }
+    throw CdcxError{CDCX_ERR_CORRUPT, "device error word " + std::to_string(e)};
   }
 };
 
@@ -299,30 +314,82 @@ int guarded(cdcx_ctx* c, F&& f) {
 
 inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
+// Grow-only page-locked host buffer.
+uint8_t* pinned(cdcx_ctx::Pinned& b, size_t bytes) {
+  if (bytes > b.cap) {
+    if (b.p) HIPCHK(hipHostFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 20);
+    if (hipHostMalloc(reinterpret_cast<void**>(&b.p), want, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      b.p = nullptr;
+      throw CdcxError{CDCX_ERR_NOMEM, "pinned host allocation of " + std::to_string(want) + " bytes failed"};
+    }
+    b.cap = want;
+  }
+  return b.p;
+}
+
+// Several small device arrays read back with one wait, through page-locked memory.
+struct Mail {
+  cdcx_ctx* c;
+  hipStream_t s;
+  uint8_t* p;
+  size_t used = 0, cap;
+  Mail(cdcx_ctx* c_, hipStream_t s_, size_t bytes) : c(c_), s(s_), cap(bytes + 64) { p = pinned(c->pin_mail, cap); }
+  size_t add(const void* d, size_t bytes) {
+    const size_t off = (used + 7) & ~size_t(7);
+    if (off + bytes > cap) throw CdcxError{CDCX_ERR_ARG, "read-back buffer too small"};
+    if (bytes) HIPCHK(hipMemcpyAsync(p + off, d, bytes, hipMemcpyDeviceToHost, s));
+    used = off + bytes;
+    return off;
+  }
+  const uint8_t* wait() {
+    c->collect(s);
+    return p;
+  }
+};
+inline void raise_device_error(uint32_t e) { cdcx_ctx::raise_device_error(e); }
+
+// Units of the last encode on the host (downloaded on first use).
+const std::vector<Unit>& host_enc_units(cdcx_ctx* c, hipStream_t s) {
+  if (c->enc_units_stale) {
+    c->enc_units = c->download(c->d_enc_units, (size_t)c->n_enc_units, s);
+    c->enc_units_stale = false;
+  }
+  return c->enc_units;
+}
+
 // ---------------------------------------------------------------------------------------
 // Encode a batch of rank streams already in device memory.
 // Outputs: c->d_out with the rank files at file_off[r] (16-aligned), file_len[r].
+//
+// The work lists between the kernels (chunks, units, sort tiles, segment offsets, output
+// layout) are built on the device (lists.hip).  The host waits four times, each time for a
+// few hundred bytes: the chunk and table counts of the ranks, the unit / segment totals, the
+// chain tiers' hand-over counts, and the file offsets with the error word at the end.
 void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* rec_off_h, std::vector<int64_t>& file_off,
                   std::vector<int64_t>& file_len, hipStream_t s) {
   const int64_t N = rec_off_h[R];
   const int64_t maxl = c->max_len;
   std::vector<int64_t> rec_off(rec_off_h, rec_off_h + R + 1), nrec(R);
-  std::vector<Tile> tiles;
   std::vector<int32_t> tile0(R), ntiles(R);
+  int64_t NT = 0;
   for (int r = 0; r < R; r++) {
     nrec[r] = rec_off[r + 1] - rec_off[r];
     if (nrec[r] > INT32_MAX - 2) throw CdcxError{CDCX_ERR_LIMIT, "more than 2^31 records in one rank stream"};
-    tile0[r] = (int32_t)tiles.size();
-    for (int64_t q = 0; q < nrec[r]; q += kTile)
-      tiles.push_back(Tile{r, (int32_t)std::min<int64_t>(kTile, nrec[r] - q), rec_off[r] + q, (int32_t)(q / kTile), 0});
-    ntiles[r] = (int32_t)tiles.size() - tile0[r];
+    tile0[r] = (int32_t)NT;
+    ntiles[r] = (int32_t)((nrec[r] + kTile - 1) / kTile);
+    NT += ntiles[r];
+    if (NT > INT32_MAX) throw CdcxError{CDCX_ERR_LIMIT, "too many records in one batch"};
   }
-  const int64_t NT = (int64_t)tiles.size();
   int64_t* d_rec_off = c->upload("rec_off", rec_off, s);
   int64_t* d_nrec = c->upload("nrec", nrec, s);
-  Tile* d_tiles = c->upload("tiles", tiles, s);
   int32_t* d_tile0 = c->upload("tile0", tile0, s);
   int32_t* d_ntiles = c->upload("ntiles", ntiles, s);
+  Tile* d_tiles = c->buf<Tile>("tiles", NT);
+  c->launch(K_LISTS, k_build_tiles, dim3(R), dim3(256), s, (const int64_t*)d_rec_off, (const int32_t*)d_tile0, d_tiles);
   uint32_t* d_err = c->buf<uint32_t>("err", 1);
   HIPCHK(hipMemsetAsync(d_err, 0, 4, s));
 
@@ -365,103 +432,109 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   c->launch(K_CHUNKS, k_chunks, dim3(R), dim3(64), s, d_rec, (const int64_t*)d_rec_off, (const int64_t*)d_nrec,
             (const int32_t*)d_p0, (const uint8_t*)d_inc0, (const int32_t*)d_t2s, (const int32_t*)d_tstart,
             (const int32_t*)d_nsets, (const int64_t*)d_ccap, maxl, d_chunk_cap, d_nchunks);
-  c->check_err(d_err, s);
-  std::vector<int32_t> nsets = c->download(d_nsets, R, s);
-  std::vector<int32_t> setlist = c->download(d_setlist, (size_t)R * kMaxSets, s);
-  std::vector<int32_t> nchunks = c->download(d_nchunks, R, s);
-  std::vector<int2> chunk_cap = c->download(d_chunk_cap, ccap_off[R], s);
 
-  // Chunks and units (host bookkeeping over a few thousand entries).
-  std::vector<Chunk> chunks;
-  std::vector<int64_t> lb_off;
-  int64_t lbn = 0;
-  for (int r = 0; r < R; r++) {
-    for (int k = 0; k < nchunks[r]; k++) {
-      const int2 se = chunk_cap[ccap_off[r] + k];
-      chunks.push_back(Chunk{r, se.x, se.y, 0, 0, 0, 0, 0});
-      lb_off.push_back(lbn);
-      lbn += nsets[r];
+  // Wait 1: tables and chunks per rank -> number of chunks and of (chunk, table) slots.
+  std::vector<int32_t> cbase(R + 1, 0);
+  std::vector<int64_t> lbase(R + 1, 0);
+  {
+    Mail m(c, s, 64 + 8 * (size_t)R);
+    const size_t o_err = m.add(d_err, 4), o_ns = m.add(d_nsets, 4 * (size_t)R), o_nc = m.add(d_nchunks, 4 * (size_t)R);
+    const uint8_t* h = m.wait();
+    raise_device_error(*reinterpret_cast<const uint32_t*>(h + o_err));
+    const int32_t* nsets = reinterpret_cast<const int32_t*>(h + o_ns);
+    const int32_t* nchunks = reinterpret_cast<const int32_t*>(h + o_nc);
+    for (int r = 0; r < R; r++) {
+      if ((int64_t)cbase[r] + nchunks[r] > INT32_MAX) throw CdcxError{CDCX_ERR_LIMIT, "too many chunks in one batch"};
+      cbase[r + 1] = cbase[r] + nchunks[r];
+      lbase[r + 1] = lbase[r] + (int64_t)nchunks[r] * nsets[r];
     }
   }
-  const int32_t C = (int32_t)chunks.size();
-  Chunk* d_chunks = c->upload("chunks", chunks, s);
-  int64_t* d_lb_off = c->upload("lb_off", lb_off, s);
+  const int32_t C = cbase[R];
+  const int64_t lbn = lbase[R];  // upper bound of the unit count: empty tables of a chunk are skipped
+  if (lbn > INT32_MAX) throw CdcxError{CDCX_ERR_LIMIT, "too many tables in one batch"};
+  int32_t* d_cbase = c->upload("cbase", cbase, s);
+  int64_t* d_lbase = c->upload("lbase", lbase, s);
+  Chunk* d_chunks = c->buf<Chunk>("chunks", C);
+  int64_t* d_lb_off = c->buf<int64_t>("lb_off", C);
   int2* d_lohi = c->buf<int2>("lohi", lbn);
-  c->launch(K_UNITS_LB, k_units_lb, dim3(C), dim3(256), s, (const Chunk*)d_chunks, C, (const int64_t*)d_lb_off,
-            (const int32_t*)d_nsets, (const int32_t*)d_tstart, (const int64_t*)d_rec_off, (const int32_t*)d_t2s, d_lohi);
-  std::vector<int2> lohi = c->download(d_lohi, lbn, s);
-  std::vector<Unit> units;
-  std::vector<int64_t> w1;
-  int64_t w1n = 0;
-  std::vector<int32_t> ufirst(R, 0), nunits(R, 0);
-  for (int32_t ci = 0; ci < C; ci++) {
-    Chunk& ch = chunks[ci];
-    ch.first_unit = (int32_t)units.size();
-    if (ci == 0 || chunks[ci - 1].rank != ch.rank) ufirst[ch.rank] = ch.first_unit;
-    for (int t = 0; t < nsets[ch.rank]; t++) {
-      const int2 lh = lohi[lb_off[ci] + t];
-      if (lh.y <= lh.x) continue;
-      Unit u{};
-      u.a = rec_off[ch.rank] + lh.x;
-      u.n = lh.y - lh.x;
-      u.rank = ch.rank;
-      u.chunk = ci;
-      u.set_id = setlist[(size_t)ch.rank * kMaxSets + t];
-      units.push_back(u);
-      w1.push_back(w1n);
-      w1n += u.n + 1;
-    }
-    ch.n_units = (int32_t)units.size() - ch.first_unit;
-    nunits[ch.rank] += ch.n_units;
-  }
-  const int32_t NU = (int32_t)units.size();
-  Unit* d_units = c->upload("units", units, s);
-  int64_t* d_w1 = c->upload("w1", w1, s);
+  int32_t* d_ucnt = c->buf<int32_t>("ucnt", C);
+  int64_t* d_uw = c->buf<int64_t>("uw", C);
+  int64_t* d_cw1 = c->buf<int64_t>("cw1", C);
+  int32_t* d_ufirst = c->buf<int32_t>("ufirst", R);
+  int32_t* d_nunits = c->buf<int32_t>("nunits", R);
+  EncTotals* d_tot = c->buf<EncTotals>("enc_totals", 1);
+  HIPCHK(hipMemsetAsync(d_tot, 0, sizeof(EncTotals), s));
+  // Units past the batch's count stay all-zero: the per-unit kernels before the count is
+  // known run over `lbn` units and find nothing to do in those.
+  Unit* d_units = c->buf<Unit>("units", lbn);
+  HIPCHK(hipMemsetAsync(d_units, 0, (size_t)lbn * sizeof(Unit), s));
+  int64_t* d_w1 = c->buf<int64_t>("w1", lbn);
+  c->launch(K_LISTS, k_build_chunks, dim3(R), dim3(256), s, (const int2*)d_chunk_cap, (const int64_t*)d_ccap,
+            (const int32_t*)d_nchunks, (const int32_t*)d_nsets, (const int32_t*)d_cbase, (const int64_t*)d_lbase, d_chunks,
+            d_lb_off);
+  c->launch(K_UNITS_LB, k_units_lb, dim3(C), dim3(kMaxSets), s, (const Chunk*)d_chunks, C, (const int64_t*)d_lb_off,
+            (const int32_t*)d_nsets, (const int32_t*)d_tstart, (const int64_t*)d_rec_off, (const int32_t*)d_t2s, d_lohi,
+            d_ucnt, d_uw);
+  c->launch(K_LISTS, k_scan_chunks, dim3(1), dim3(1024), s, d_chunks, C, (const int32_t*)d_ucnt, (const int64_t*)d_uw,
+            (const int32_t*)d_cbase, R, d_ufirst, d_nunits, d_cw1, d_tot);
+  c->launch(K_LISTS, k_fill_units, dim3(C), dim3(kMaxSets), s, (const Chunk*)d_chunks, (const int64_t*)d_lb_off,
+            (const int2*)d_lohi, (const int32_t*)d_nsets, (const int32_t*)d_setlist, (const int64_t*)d_rec_off,
+            (const int64_t*)d_cw1, d_units, d_w1);
   uint64_t* d_mkey = c->buf<uint64_t>("mkey", N);
   int32_t* d_midx = c->buf<int32_t>("midx", N);
   int32_t* d_wp = c->buf<int32_t>("wp", N);
   int32_t* d_run_id = c->buf<int32_t>("run_id", N);
   uint64_t* d_run_cnt = c->buf<uint64_t>("run_cnt", N);
-  c->launch(K_UNIT_PREP, k_unit_prep, dim3(NU), dim3(256), s, d_units, (const TRec*)d_trec, d_mkey, d_midx, d_wp, d_run_id,
-            d_run_cnt, d_err);
-  c->check_err(d_err, s);
-  units = c->download(d_units, NU, s);
+  c->launch(K_UNIT_PREP, k_unit_prep, dim3((unsigned)lbn), dim3(256), s, d_units, (const TRec*)d_trec, d_mkey, d_midx, d_wp,
+            d_run_id, d_run_cnt, d_err);
 
   // Clock-order rank: the windowed pass for every unit (tiles of kSortTile events); the units
-  // it flags (wfail) are ranked again by the tile sort after the next download, then get
-  // their epoch line and cuts (both skip flagged units until then).
-  std::vector<SortTile> st;
-  for (int32_t u = 0; u < NU; u++) {
-    units[u].sort_tile0 = (int32_t)st.size();
-    units[u].wfail = c->rank_tier > 0 ? 1 : 0;
-    for (int32_t q = 0; q * kSortTile < units[u].M; q++) st.push_back(SortTile{u, q});
-  }
-  const int64_t NS = (int64_t)st.size();
-  d_units = c->upload("units", units, s);
-  SortTile* d_st = c->upload("sort_tiles", st, s);
+  // it flags (wfail) are ranked again by the tile sort after the next wait, then get their
+  // epoch line and cuts (both skip flagged units until then).
+  c->launch(K_LISTS, k_units_scan_prep, dim3(1), dim3(1024), s, d_units, (int32_t)c->rank_tier, d_tot);
+  const int64_t NSmax = N / kSortTile + lbn;  // >= sum of ceil(M / kSortTile)
+  SortTile* d_st = c->buf<SortTile>("sort_tiles", NSmax);
+  HIPCHK(hipMemsetAsync(d_st, 0xFF, (size_t)NSmax * sizeof(SortTile), s));  // unit -1: no tile
+  c->launch(K_LISTS, k_fill_sort_tiles, dim3((unsigned)lbn), dim3(256), s, (const Unit*)d_units, d_st);
   int32_t* d_cord = c->buf<int32_t>("cord", N);
   int32_t* d_inv = c->buf<int32_t>("inv", N);
   uint64_t* d_skey = c->buf<uint64_t>("skey", N);
   if (c->rank_tier == 0)
-    c->launch(K_WINDOW_RANK, k_window_rank, dim3(NS), dim3(256), s, d_units, (const SortTile*)d_st,
+    c->launch(K_WINDOW_RANK, k_window_rank, dim3((unsigned)NSmax), dim3(256), s, d_units, (const SortTile*)d_st,
               (const uint64_t*)d_mkey, d_cord, d_inv, d_skey);
   uint64_t* d_ep_rank = c->buf<uint64_t>("ep_rank", N);
   uint64_t* d_ep_clk = c->buf<uint64_t>("ep_clk", N);
   int32_t* d_segend = c->buf<int32_t>("segend", N);
-  int32_t* d_opn = c->buf<int32_t>("opn", N);  // first untaken column of every row (k_cuts)
-  auto epoch_cuts = [&]() {
-    c->launch(K_EPOCH, k_epoch<512>, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, d_err);
-    // Chain: closed-prefix segments simulated independently, then stitched (chain.hip).
-    c->launch(K_CUTS, k_cuts, dim3(NU), dim3(256), s, d_units, (const int32_t*)d_inv, d_segend, d_opn);
-    c->check_err(d_err, s);
-    units = c->download(d_units, NU, s);
+  int32_t* d_opn = c->buf<int32_t>("opn", N);  // column + open flag of every row (k_cuts)
+  int64_t* d_bound = c->buf<int64_t>("fbound", R);
+  EncTotals tot{};
+  std::vector<int64_t> bound(R, 0);
+  // Wait 2 (again after the rare re-rank / big-epoch detours): totals and epoch sources per rank.
+  auto totals = [&]() {
+    HIPCHK(hipMemsetAsync(d_bound, 0, 8 * (size_t)R, s));
+    c->launch(K_LISTS, k_units_scan_cuts, dim3(1), dim3(1024), s, d_units, d_bound, d_tot);
+    Mail m(c, s, 64 + sizeof(EncTotals) + 8 * (size_t)R);
+    const size_t o_err = m.add(d_err, 4), o_tot = m.add(d_tot, sizeof(EncTotals)), o_b = m.add(d_bound, 8 * (size_t)R);
+    const uint8_t* h = m.wait();
+    raise_device_error(*reinterpret_cast<const uint32_t*>(h + o_err));
+    memcpy(&tot, h + o_tot, sizeof(tot));
+    memcpy(bound.data(), h + o_b, 8 * (size_t)R);
   };
-  epoch_cuts();
-  std::vector<SortTile> fst;
-  for (int32_t u = 0; u < NU; u++)
-    if (units[u].wfail)
-      for (int32_t q = 0; q * kSortTile < units[u].M; q++) fst.push_back(SortTile{u, q});
-  if (!fst.empty()) {
+  auto epoch_cuts = [&](unsigned grid) {
+    c->launch(K_EPOCH, k_epoch<512>, dim3(grid), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, d_err);
+    // Chain: closed-prefix segments simulated independently, then stitched (chain.hip).
+    c->launch(K_CUTS, k_cuts, dim3(grid), dim3(256), s, d_units, (const int32_t*)d_inv, d_segend, d_opn);
+    totals();
+  };
+  epoch_cuts((unsigned)lbn);
+  const int32_t NU = tot.n_units;
+  const int64_t NS = tot.n_sort_tiles;
+  if (tot.n_fail > 0) {
+    std::vector<Unit> units = c->download(d_units, NU, s);
+    std::vector<SortTile> fst;
+    for (int32_t u = 0; u < NU; u++)
+      if (units[u].wfail)
+        for (int32_t q = 0; q * kSortTile < units[u].M; q++) fst.push_back(SortTile{u, q});
     SortTile* d_fst = c->upload("sort_tiles_fb", fst, s);
     uint64_t* d_tkey = c->buf<uint64_t>("tkey", N);
     int32_t* d_lrank = c->buf<int32_t>("lrank", N);
@@ -473,19 +546,38 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
               (const uint64_t*)d_tmm, d_cord, d_inv, d_skey);
     for (Unit& u : units) u.wfail = u.wfail ? 0 : 2;  // epoch and cuts for the re-ranked units only
     d_units = c->upload("units", units, s);
-    epoch_cuts();
+    c->launch(K_EPOCH, k_epoch<512>, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, d_err);
+    c->launch(K_CUTS, k_cuts, dim3(NU), dim3(256), s, d_units, (const int32_t*)d_inv, d_segend, d_opn);
+    c->launch(K_LISTS, k_units_clear_wfail, dim3(blocks(NU, 256)), dim3(256), s, d_units, NU);
+    totals();
   }
-  for (Unit& u : units) u.wfail = 0;
-  int64_t nsegs = 0;
-  for (Unit& u : units) {
-    u.seg0 = (int32_t)nsegs;
-    nsegs += u.nseg;
-  }
-  if (nsegs > INT32_MAX) throw CdcxError{CDCX_ERR_LIMIT, "too many segments in one batch"};
-  d_units = c->upload("units", units, s);
-  if (std::any_of(units.begin(), units.end(), [](const Unit& u) { return u.S == -1; }))  // > 256 sources
+  if (tot.n_big > 0) {  // > 256 sources in some table
     c->launch(K_EPOCH, k_epoch<2 * kMaxUnitSources>, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank,
               d_ep_clk, d_err);
+    totals();
+  }
+  const int64_t nsegs = tot.n_segs;
+  if (nsegs > INT32_MAX) throw CdcxError{CDCX_ERR_LIMIT, "too many segments in one batch"};
+  const int64_t key_run = tot.matched;
+
+  // Footer scratch and order: needs the epoch lines only, so it runs ahead of the chain.
+  std::vector<int64_t> fk_off(R + 1, 0), fb_off(R + 1, 0);
+  int64_t foot_max = 0;
+  for (int r = 0; r < R; r++) {
+    fk_off[r + 1] = fk_off[r] + bound[r] + 1;
+    fb_off[r + 1] = fb_off[r] + (int64_t)hash_bucket_capacity((uint64_t)bound[r]) + 1;
+    foot_max += 20 + 4 * bound[r] + 16;
+  }
+  int64_t* d_fk_off = c->upload("fk_off", fk_off, s);
+  int64_t* d_fb_off = c->upload("fb_off", fb_off, s);
+  uint64_t* d_fkey = c->buf<uint64_t>("fkey", fk_off[R]);
+  int32_t* d_fnext = c->buf<int32_t>("fnext", fk_off[R]);
+  int32_t* d_fbucket = c->buf<int32_t>("fbucket", fb_off[R]);
+  int32_t* d_fcount = c->buf<int32_t>("fcount", R);
+  c->launch(K_FOOTER_ORDER, k_footer_order, dim3(R), dim3(256), s, (const Unit*)d_units,
+            (const int32_t*)d_ufirst, (const int32_t*)d_nunits, (const uint64_t*)d_ep_rank, R, (const int64_t*)d_fk_off,
+            (const int64_t*)d_fb_off, d_fkey, d_fnext, d_fbucket, d_fcount);
+
   int32_t* d_pid = nullptr;
   int32_t* d_pdl = nullptr;
   if (!c->rep) {  // the rep encoder writes no matched-event sections: no chain, no edit sequence
@@ -503,9 +595,9 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int32_t* d_topg = c->buf<int32_t>("topg", N);
   int32_t* d_qn = c->buf<int32_t>("qn", N);
   uint8_t* d_chain = c->buf<uint8_t>("chain", N);  // every row written by k_chain_mark
-  // Tiers: 16-lane groups; segments whose leaf list outgrows 16 slots go to 64-lane groups,
-  // then to the lane kernel's exact global-memory path.  Each tier rewrites every output of
-  // the segments it takes.
+  // Tiers: 8-lane groups with 16 leaf slots; segments whose leaf list outgrows them go to
+  // 64-lane groups, then to the lane kernel's exact global-memory path.  Each tier rewrites
+  // every output of the segments it takes.
   int32_t* d_cnt = c->buf<int32_t>("chain_cnt", 4);
   int32_t* d_ovf1 = c->buf<int32_t>("chain_ovf1", nsegs);
   int32_t* d_ovf2 = c->buf<int32_t>("chain_ovf2", nsegs);
@@ -531,7 +623,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
       nlist = d_cnt + 1;
     }
     // The 64-lane tier reads its segment count from the device (d_cnt + 1), so the host
-    // waits once, after it; only the rare lane tier needs the count on the host.
+    // waits once, after it (wait 3); only the rare lane tier needs the count on the host.
     if (c->chain_tier <= 1) {
       const int64_t g64 = c->chain_tier <= 0 ? std::min<int64_t>(1024, blocks(nsegs, 4)) : blocks(n, 4);
       c->launch(K_CHAIN_G64, k_chain_grp<64>, dim3((unsigned)std::max<int64_t>(1, g64)), dim3(256), s,
@@ -540,12 +632,14 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
       list = d_ovf2;
     }
     {
-      const std::vector<int32_t> cnt = c->download(d_cnt, 3, s);
+      Mail m(c, s, 64);
+      const size_t o = m.add(d_cnt, 12);
+      const int32_t* cnt = reinterpret_cast<const int32_t*>(m.wait() + o);
       c->chain_tier_counts[0] = nsegs;
       c->chain_tier_counts[1] = c->chain_tier <= 0 ? cnt[1] : nsegs;
       if (c->chain_tier <= 1) n = cnt[2];
     }
-    int2* d_leaves = n > 0 ? c->buf<int2>("leaves", w1n) : nullptr;  // lane tier only
+    int2* d_leaves = n > 0 ? c->buf<int2>("leaves", tot.w1n) : nullptr;  // lane tier only
     if (n > 0)
       c->launch(K_CHAIN_SEG, k_chain_seg<16>, dim3((unsigned)std::min<int64_t>(1024, blocks(n, 256))), dim3(256), s,
                 (const Unit*)d_units, d_segs, (int32_t)n, list, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par,
@@ -573,88 +667,55 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   d_pdl = c->buf<int32_t>("pdl", N);
   c->launch(K_DELTAS, k_deltas, dim3(NU), dim3(256), s, (const Unit*)d_units, (const uint32_t*)d_seq, (const int32_t*)d_sx,
             d_pid, d_pdl);
-  c->check_err(d_err, s);
-  units = c->download(d_units, NU, s);
   }
 
-  // Sizes, footer scratch, offsets.
-  std::vector<int64_t> fk_off(R + 1, 0), fb_off(R + 1, 0);
-  {
-    std::vector<int64_t> bound(R, 0);
-    for (const Unit& u : units) bound[u.rank] += u.S;
-    for (int r = 0; r < R; r++) {
-      fk_off[r + 1] = fk_off[r] + bound[r] + 1;
-      fb_off[r + 1] = fb_off[r] + (int64_t)hash_bucket_capacity((uint64_t)bound[r]) + 1;
-    }
-  }
-  int64_t key_run = 0;
-  for (Unit& u : units) {
-    u.key_off = key_run;
-    key_run += u.M;
-  }
-  d_units = c->upload("units", units, s);
-  int32_t* d_ufirst = c->upload("ufirst", ufirst, s);
-  int32_t* d_nunits = c->upload("nunits", nunits, s);
-  int64_t* d_fk_off = c->upload("fk_off", fk_off, s);
-  int64_t* d_fb_off = c->upload("fb_off", fb_off, s);
-  uint64_t* d_fkey = c->buf<uint64_t>("fkey", fk_off[R]);
-  int32_t* d_fnext = c->buf<int32_t>("fnext", fk_off[R]);
-  int32_t* d_fbucket = c->buf<int32_t>("fbucket", fb_off[R]);
-  int32_t* d_fcount = c->buf<int32_t>("fcount", R);
-  c->launch(K_FOOTER_ORDER, k_footer_order, dim3(R), dim3(256), s, (const Unit*)d_units,
-            (const int32_t*)d_ufirst, (const int32_t*)d_nunits, (const uint64_t*)d_ep_rank, R, (const int64_t*)d_fk_off,
-            (const int64_t*)d_fb_off, d_fkey, d_fnext, d_fbucket, d_fcount);
-  std::vector<int32_t> fcount = c->download(d_fcount, R, s);
-
-  file_off.assign(R, 0);
-  file_len.assign(R, 0);
-  std::vector<int64_t> foot_off(R, 0);
-  int64_t pos = 0;
-  size_t ui = 0;
-  int32_t ci = 0;
-  for (int r = 0; r < R; r++) {
-    pos = align_up(pos, 16);
-    file_off[r] = pos;
-    for (; ci < C && chunks[ci].rank == r; ci++) {
-      Chunk& ch = chunks[ci];
-      ch.out_off = pos;
-      int64_t q = pos + 8;
-      for (int32_t k = 0; k < ch.n_units; k++, ui++) {
-        Unit& u = units[ui];
-        u.out_off = q;
-        q += 72 + 16ll * u.S + (c->rep ? 0 : 8ll * u.W + 8ll * u.M + 16ll * u.U + 8ll * u.P);
-      }
-      ch.payload = q - pos - 8;
-      pos = q;
-    }
-    foot_off[r] = pos;
-    pos += 20 + 4ll * fcount[r];
-    file_len[r] = pos - file_off[r];
-  }
-  const int64_t total = align_up(pos, 16);
-  d_units = c->upload("units", units, s);
-  d_chunks = c->upload("chunks", chunks, s);
-  int64_t* d_foot = c->upload("foot_off", foot_off, s);
-  uint8_t* d_out = c->buf<uint8_t>("out", total);
+  // Output layout on the device.  The output buffer is sized before the pair counts are
+  // known, for P = M in every unit (a few bytes per record more than the files take).
+  const int64_t total_max = 8ll * C + 72ll * NU + 16ll * tot.sources + foot_max +
+                            (c->rep ? 0 : 8ll * tot.with_next + 16ll * tot.matched + 16ll * tot.runs);
+  uint8_t* d_out = c->buf<uint8_t>("out", total_max);
   int2* d_keys = c->buf<int2>("keys", key_run);
+  int64_t* d_upre = c->buf<int64_t>("upre", (size_t)NU + 1);
+  int64_t* d_cpre = c->buf<int64_t>("cpre", (size_t)C + 1);
+  int64_t* d_files = c->buf<int64_t>("file_layout", 3 * (size_t)R + 1);  // file_off[R], file_len[R], foot_off[R], total
+  c->launch(K_LISTS, k_out_layout, dim3(1), dim3(1024), s, d_units, d_chunks, C, (const int32_t*)d_cbase, R,
+            (const int32_t*)d_fcount, (int32_t)c->rep, (const EncTotals*)d_tot, d_upre, d_cpre, d_files, d_files + R,
+            d_files + 2 * R, d_files + 3 * R);
   c->launch(K_WRITE_UNITS, k_write_units, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_midx,
             (const int32_t*)d_wp, (const int32_t*)d_run_id, (const uint64_t*)d_run_cnt, (const uint64_t*)d_ep_rank,
             (const uint64_t*)d_ep_clk, (const int32_t*)d_pid, (const int32_t*)d_pdl, (int32_t)c->rep, d_out);
   c->launch(K_CHUNK_HEADERS, k_chunk_headers, dim3(blocks(C, 256)), dim3(256), s, (const Chunk*)d_chunks, C, d_out);
   c->launch(K_FOOTER_WRITE, k_footer_write, dim3(blocks(R, 64)), dim3(64), s, (const int64_t*)d_fk_off,
             (const int64_t*)d_fb_off, (const uint64_t*)d_fkey, (const int32_t*)d_fnext, (const int32_t*)d_fbucket,
-            (const int32_t*)d_fcount, (const int64_t*)d_foot, R, d_out);
+            (const int32_t*)d_fcount, (const int64_t*)(d_files + 2 * R), R, d_out);
   c->launch(K_WRITE_KEYS, k_write_keys, dim3(NU), dim3(256), s, (const Unit*)d_units, (const uint64_t*)d_skey, d_keys);
-  c->check_err(d_err, s);
+  {  // wait 4: error word, file offsets and lengths
+    Mail m(c, s, 64 + 8 * (3 * (size_t)R + 1));
+    const size_t o_err = m.add(d_err, 4), o_f = m.add(d_files, 8 * (3 * (size_t)R + 1));
+    const uint8_t* h = m.wait();
+    raise_device_error(*reinterpret_cast<const uint32_t*>(h + o_err));
+    const int64_t* f = reinterpret_cast<const int64_t*>(h + o_f);
+    file_off.assign(f, f + R);
+    file_len.assign(f + R, f + 2 * R);
+    if (f[3 * R] > total_max) throw CdcxError{CDCX_ERR_CORRUPT, "output layout exceeds its bound"};
+  }
   c->d_out = d_out;
   c->d_keys = d_keys;
   c->n_keys = key_run;
-  c->enc_units = units;
+  c->d_enc_units = d_units;
+  c->n_enc_units = NU;
+  c->enc_units.clear();
+  c->enc_units_stale = true;
   c->enc_rec_off = rec_off;
 }
 
 // ---------------------------------------------------------------------------------------
 // Decode a batch of rank files in device memory (d_in; file r at off[r], len[r], 8-aligned).
+//
+// The chunk, unit, launch-order and record-tile lists are built on the device (lists.hip); the
+// host waits for the chunk counts, the unit count, the scratch totals, the first tier's failure
+// count and the error word -- a few words each -- and fetches the unit table itself only when
+// a caller asks for the decoded tables (host_dec_units).
 void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector<int64_t>& off,
                   const std::vector<int64_t>& len, const int2* d_keys, int64_t n_keys, bool records, hipStream_t s) {
   for (int r = 0; r < R; r++)
@@ -666,50 +727,60 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   int32_t* d_nch = c->buf<int32_t>("d_nchunks", R);
   c->launch(K_DEC_COUNT_CHUNKS, k_dec_count_chunks, dim3(blocks(R, 64)), dim3(64), s, d_in, (const int64_t*)d_off,
             (const int64_t*)d_len, R, d_nch, d_err);
-  c->check_err(d_err, s);
-  std::vector<int32_t> nch = c->download(d_nch, R, s), cbase(R, 0);
-  int32_t C = 0;
-  for (int r = 0; r < R; r++) {
-    cbase[r] = C;
-    C += nch[r];
+  std::vector<int32_t> cbase(R + 1, 0);
+  {
+    Mail m(c, s, 64 + 4 * (size_t)R);
+    const size_t o_err = m.add(d_err, 4), o_n = m.add(d_nch, 4 * (size_t)R);
+    const uint8_t* h = m.wait();
+    raise_device_error(*reinterpret_cast<const uint32_t*>(h + o_err));
+    const int32_t* nch = reinterpret_cast<const int32_t*>(h + o_n);
+    for (int r = 0; r < R; r++) {
+      if ((int64_t)cbase[r] + nch[r] > INT32_MAX) throw CdcxError{CDCX_ERR_LIMIT, "too many chunks in one batch"};
+      cbase[r + 1] = cbase[r] + nch[r];
+    }
   }
+  const int32_t C = cbase[R];
   int32_t* d_cbase = c->upload("d_cbase", cbase, s);
   c->dcbase = cbase;
-  c->dcbase.push_back(C);
   DChunk* d_ch = c->buf<DChunk>("d_chunks", C);
   c->launch(K_DEC_LIST_CHUNKS, k_dec_list_chunks, dim3(blocks(R, 64)), dim3(64), s, d_in, (const int64_t*)d_off,
             (const int32_t*)d_cbase, (const int32_t*)d_nch, R, d_ch);
   int32_t* d_nu = c->buf<int32_t>("d_nunits", C);
+  int32_t* d_fu = c->buf<int32_t>("d_first_unit", C);
+  DecTotals* d_tot = c->buf<DecTotals>("dec_totals", 1);
+  HIPCHK(hipMemsetAsync(d_tot, 0, sizeof(DecTotals), s));
   c->launch(K_DEC_UNITS, k_dec_units, dim3(blocks(C, 64)), dim3(64), s, d_in, (const DChunk*)d_ch, C,
             (const int32_t*)nullptr, d_nu, (DUnit*)nullptr, d_err);
-  c->check_err(d_err, s);
-  c->dnunits = c->download(d_nu, C, s);
-  c->dfirst_unit.assign(C, 0);
-  int32_t NU = 0;
-  for (int32_t k = 0; k < C; k++) {
-    c->dfirst_unit[k] = NU;
-    NU += c->dnunits[k];
-  }
-  int32_t* d_fu = c->upload("d_first_unit", c->dfirst_unit, s);
+  c->launch(K_LISTS, k_dec_scan_chunks, dim3(1), dim3(1024), s, (const int32_t*)d_nu, C, d_fu, d_tot);
+  DecTotals tot{};
+  auto totals = [&]() {
+    Mail m(c, s, 64 + sizeof(DecTotals));
+    const size_t o_err = m.add(d_err, 4), o_t = m.add(d_tot, sizeof(DecTotals));
+    const uint8_t* h = m.wait();
+    raise_device_error(*reinterpret_cast<const uint32_t*>(h + o_err));
+    memcpy(&tot, h + o_t, sizeof(tot));
+  };
+  totals();
+  if (tot.n_units > INT32_MAX) throw CdcxError{CDCX_ERR_LIMIT, "too many tables in one batch"};
+  const int32_t NU = (int32_t)tot.n_units;
   DUnit* d_units = c->buf<DUnit>("d_units", NU);
+  int32_t* d_rt0 = c->buf<int32_t>("d_rec_tile0", (size_t)NU + 1);
   c->launch(K_DEC_UNITS, k_dec_units, dim3(blocks(C, 64)), dim3(64), s, d_in, (const DChunk*)d_ch, C, (const int32_t*)d_fu,
             (int32_t*)nullptr, d_units, d_err);
-  c->check_err(d_err, s);
-  c->dchunks = c->download(d_ch, C, s);
-  std::vector<DUnit> units = c->download(d_units, NU, s);
-  int64_t wb = 0, ro = 0, ko = 0;
-  for (DUnit& u : units) {
-    u.wbase = wb;
-    u.rec_off = ro;
-    u.key_off = ko;
-    wb += (int64_t)u.M + 1;
-    ro += (int64_t)u.M + (u.Uc > 0 ? u.U : 0);
-    ko += u.M;
-    u.fb = std::min(std::max(c->dec_tier, 0), 2);
-  }
+  c->launch(K_LISTS, k_dec_scan_units, dim3(1), dim3(1024), s, d_units, NU, (int32_t)std::min(std::max(c->dec_tier, 0), 2),
+            d_rt0, d_tot);
+  totals();
+  const int64_t wb = tot.rows, ro = tot.records, ko = tot.keys;
   if (records && n_keys < ko) throw CdcxError{CDCX_ERR_ARG, "fewer sorted keys than matched events in the files"};
-  d_units = c->upload("d_units", units, s);
-  c->dunits = units;
+  c->d_dunits = d_units;
+  c->d_dchunks = d_ch;
+  c->d_dnunits = d_nu;
+  c->d_dfirst_unit = d_fu;
+  c->n_dunits = NU;
+  c->n_dchunks = C;
+  c->dec_host_stale = true;
+  c->dec_stream = s;
+  c->dunits.clear();
   uint64_t* d_wpd = c->buf<uint64_t>(kAliasWpd, wb);
   uint64_t* d_uidd = c->buf<uint64_t>(kAliasUidd, wb);
   uint64_t* d_idd = c->buf<uint64_t>(kAliasIdd, wb);  // written by k_dec_perm_grp
@@ -725,15 +796,29 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   int32_t* d_cinv = c->buf<int32_t>(kAliasCinv, ko);
   int32_t* d_nfail = c->buf<int32_t>("d_nfail", 2);
   HIPCHK(hipMemsetAsync(d_nfail, 0, 8, s));
-  {
-    std::vector<int32_t> order(NU);
-    for (int32_t i = 0; i < NU; i++) order[i] = i;
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return units[a].P > units[b].P; });
-    int32_t* d_order = c->upload("d_perm_order", order, s);
-    c->launch(K_DEC_WIN1, k_dec_perm_grp, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order, NU, d_in,
-              d_idd, d_dld, d_perm, d_cinv, d_nfail);
+  int32_t* d_order = c->buf<int32_t>("d_perm_order", NU);
+  c->launch(K_LISTS, k_dec_order, dim3(blocks(NU, 256)), dim3(256), s, (const DUnit*)d_units, NU, d_order);
+  c->launch(K_DEC_WIN1, k_dec_perm_grp, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order, NU, d_in,
+            d_idd, d_dld, d_perm, d_cinv, d_nfail);
+  // The record tiles are listed while the rebuild runs; the reconstruction itself is launched
+  // before the wait for the failure count when no unit can have failed into a later tier.
+  int2* d_rt = nullptr;
+  int32_t* d_recs = nullptr;
+  if (records) {
+    d_rt = c->buf<int2>("d_rec_tiles", tot.rec_tiles);
+    d_recs = c->buf<int32_t>(kAliasRecs, 8 * ro);
+    c->launch(K_LISTS, k_dec_fill_tiles, dim3(NU), dim3(256), s, (const DUnit*)d_units, (const int32_t*)d_rt0, d_rt);
   }
-  int32_t nf = c->dec_tier > 0 ? NU : c->download(d_nfail, 1, s)[0];
+  // An input the kernels flagged must not reach the record reconstruction (it trusts the
+  // sections' checks and the permutation): the error word travels with the failure count.
+  int32_t nf = NU;
+  {
+    Mail m(c, s, 64);
+    const size_t o_err = m.add(d_err, 4), o = m.add(d_nfail, 4);
+    const uint8_t* h = m.wait();
+    raise_device_error(*reinterpret_cast<const uint32_t*>(h + o_err));
+    if (c->dec_tier <= 0) nf = *reinterpret_cast<const int32_t*>(h + o);
+  }
   if (nf > 0) {
     c->launch(K_DEC_WIN4, k_dec_perm_window<4>, dim3(NU), dim3(64), s, d_units, NU, 1, (const uint64_t*)d_idd,
               (const uint64_t*)d_dld, d_perm, d_nfail + 1);
@@ -746,49 +831,32 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
     }
     c->launch(K_DEC_PERM, k_dec_cinv, dim3(NU), dim3(256), s, (const DUnit*)d_units, (const int32_t*)d_perm, d_cinv);
     nf = nf2;
+    c->check_err(d_err, s);
   }
   c->last_fallback_units = nf;
-  c->check_err(d_err, s);
-  units = c->download(d_units, NU, s);
-  c->dunits = units;
   c->d_perm = d_perm;
   c->n_rec_out = ro;
   if (records) {
-    std::vector<int2> rt;
-    for (int32_t q = 0; q < NU; q++) {
-      const DUnit& u = units[q];
-      if (u.M == 0 && (u.Uc == 0 || u.U == 0)) continue;
-      const int32_t nt = std::max<int32_t>(1, (u.M + 1023) / 1024);
-      for (int32_t k = 0; k < nt; k++) rt.push_back(make_int2(q, k));
-    }
-    int2* d_rt = c->upload("d_rec_tiles", rt, s);
-    int32_t* d_recs = c->buf<int32_t>(kAliasRecs, 8 * ro);
-    c->launch(K_DEC_RECORDS, k_dec_records, dim3((unsigned)rt.size()), dim3(256), s, (const DUnit*)d_units,
+    c->launch(K_DEC_RECORDS, k_dec_records, dim3((unsigned)tot.rec_tiles), dim3(256), s, (const DUnit*)d_units,
               (const int2*)d_rt, d_in, (const int32_t*)d_cinv, (const uint8_t*)d_wnf, (const uint64_t*)d_uidd, d_keys,
               (int4*)d_recs);
-    c->check_err(d_err, s);
     c->d_rec_out = d_recs;
   }
+  c->check_err(d_err, s);
+}
+
+// Unit and chunk tables of the last decode on the host (downloaded on first use).
+void host_dec_units(cdcx_ctx* c, hipStream_t s) {
+  if (!c->dec_host_stale) return;
+  c->dunits = c->download((const DUnit*)c->d_dunits, (size_t)c->n_dunits, s);
+  c->dchunks = c->download((const DChunk*)c->d_dchunks, (size_t)c->n_dchunks, s);
+  c->dnunits = c->download((const int32_t*)c->d_dnunits, (size_t)c->n_dchunks, s);
+  c->dfirst_unit = c->download((const int32_t*)c->d_dfirst_unit, (size_t)c->n_dchunks, s);
+  c->dec_host_stale = false;
 }
 
 // Host-side table dump of the last decode (tests / drop-in shim): mirrors the fields the
 // reference keeps in rempi_encoder_input_format_test_table after decode().
-uint8_t* pinned(cdcx_ctx::Pinned& b, size_t bytes) {
-  if (bytes > b.cap) {
-    if (b.p) HIPCHK(hipHostFree(b.p));
-    b.p = nullptr;
-    b.cap = 0;
-    const size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 20);
-    if (hipHostMalloc(reinterpret_cast<void**>(&b.p), want, hipHostMallocDefault) != hipSuccess) {
-      (void)hipGetLastError();
-      b.p = nullptr;
-      throw CdcxError{CDCX_ERR_NOMEM, "pinned host allocation of " + std::to_string(want) + " bytes failed"};
-    }
-    b.cap = want;
-  }
-  return b.p;
-}
-
 // The decoded per-unit arrays of the last decode, packed on the device (k_dec_pack_tables:
 // per unit with_previous[W], unmatched ids[U], ids[P], delays[P]) and copied into pinned
 // host memory with perm[] in one D2H each.
@@ -799,6 +867,7 @@ struct DecodedTables {
 };
 
 DecodedTables download_tables(cdcx_ctx* c, hipStream_t s) {
+  host_dec_units(c, s);
   const int32_t NU = (int32_t)c->dunits.size();
   DecodedTables t;
   t.pk_off.resize(NU + 1);
@@ -892,7 +961,8 @@ void dump_chunks(const cdcx_ctx* c, const DecodedTables& t, const uint8_t* in, i
 
 std::vector<int64_t> tables_dump(cdcx_ctx* c, const uint8_t* in, hipStream_t s) {
   std::vector<int64_t> d;
-  dump_chunks(c, download_tables(c, s), in, 0, (int32_t)c->dchunks.size(), d);
+  const DecodedTables tb = download_tables(c, s);  // (fetches the chunk table first)
+  dump_chunks(c, tb, in, 0, (int32_t)c->dchunks.size(), d);
   return d;
 }
 
@@ -947,6 +1017,7 @@ void cdcx_destroy(cdcx_ctx* c) {
     if (kv.second.p) (void)hipFree(kv.second.p);
   if (c->pin_in.p) (void)hipHostFree(c->pin_in.p);
   if (c->pin_tab.p) (void)hipHostFree(c->pin_tab.p);
+  if (c->pin_mail.p) (void)hipHostFree(c->pin_mail.p);
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   for (auto& p : c->pending) {
     (void)hipEventDestroy(p.a);
@@ -1413,6 +1484,8 @@ int cdcx_decode_chunk_perm_static(cdcx_ctx* c, const uint8_t* d_payload, size_t 
 
 int cdcx_decode_rank_offsets(cdcx_ctx* c, int32_t n_ranks, int64_t* rec_off, int64_t* perm_off) {
   if (!c || n_ranks < 0 || !rec_off || !perm_off || (size_t)n_ranks + 1 != c->dcbase.size()) return CDCX_ERR_ARG;
+  const int rc = guarded(c, [&] { host_dec_units(c, c->dec_stream); });
+  if (rc != CDCX_OK) return rc;
   const size_t NU = c->dunits.size(), C = c->dfirst_unit.size();
   int64_t rec_end = 0, perm_end = 0;
   if (NU) {
@@ -1435,6 +1508,8 @@ int cdcx_verify_roundtrip_device(cdcx_ctx* c, const int32_t* d_rec, int64_t* mis
   if (!c || !d_rec || !mismatches) return CDCX_ERR_ARG;
   return guarded(c, [&] {
     hipStream_t s = (hipStream_t)stream;
+    host_enc_units(c, s);
+    host_dec_units(c, s);
     const int32_t NU = (int32_t)c->enc_units.size();
     if (c->dunits.size() != c->enc_units.size())
       throw CdcxError{CDCX_ERR_ARG, "the last decode does not hold the units of the last encode"};

@@ -31,7 +31,7 @@ __global__ void k_tile_p0(const uint8_t*, const Tile*, const int32_t*, const int
 __global__ void k_chunks(const int32_t*, const int64_t*, const int64_t*, const int32_t*, const uint8_t*, const int32_t*,
                          const int32_t*, const int32_t*, const int64_t*, int64_t, int2*, int32_t*);
 __global__ void k_units_lb(const Chunk*, int32_t, const int64_t*, const int32_t*, const int32_t*, const int64_t*,
-                           const int32_t*, int2*);
+                           const int32_t*, int2*, int32_t*, int64_t*);
 __global__ void k_unit_prep(Unit*, const TRec*, uint64_t*, int32_t*, int32_t*, int32_t*, uint64_t*, uint32_t*);
 __global__ void k_window_rank(Unit*, const SortTile*, const uint64_t*, int32_t*, int32_t*, uint64_t*);
 __global__ void k_sort_tiles(const Unit*, const SortTile*, const uint64_t*, uint64_t*, int32_t*, uint64_t*);
@@ -70,6 +70,25 @@ __global__ void k_footer_order(const Unit*, const int32_t*, const int32_t*, cons
 __global__ void k_footer_write(const int64_t*, const int64_t*, const uint64_t*, const int32_t*, const int32_t*,
                                const int32_t*, const int64_t*, int32_t, uint8_t*);
 __global__ void k_write_keys(const Unit*, const uint64_t*, int2*);
+
+// lists.hip
+__global__ void k_build_tiles(const int64_t*, const int32_t*, Tile*);
+__global__ void k_build_chunks(const int2*, const int64_t*, const int32_t*, const int32_t*, const int32_t*, const int64_t*,
+                               Chunk*, int64_t*);
+__global__ void k_scan_chunks(Chunk*, int32_t, const int32_t*, const int64_t*, const int32_t*, int32_t, int32_t*, int32_t*,
+                              int64_t*, EncTotals*);
+__global__ void k_fill_units(const Chunk*, const int64_t*, const int2*, const int32_t*, const int32_t*, const int64_t*,
+                             const int64_t*, Unit*, int64_t*);
+__global__ void k_units_scan_prep(Unit*, int32_t, EncTotals*);
+__global__ void k_fill_sort_tiles(const Unit*, SortTile*);
+__global__ void k_units_scan_cuts(Unit*, int64_t*, EncTotals*);
+__global__ void k_units_clear_wfail(Unit*, int32_t);
+__global__ void k_out_layout(Unit*, Chunk*, int32_t, const int32_t*, int32_t, const int32_t*, int32_t, const EncTotals*,
+                             int64_t*, int64_t*, int64_t*, int64_t*, int64_t*, int64_t*);
+__global__ void k_dec_scan_chunks(const int32_t*, int32_t, int32_t*, DecTotals*);
+__global__ void k_dec_scan_units(DUnit*, int32_t, int32_t, int32_t*, DecTotals*);
+__global__ void k_dec_order(const DUnit*, int32_t, int32_t*);
+__global__ void k_dec_fill_tiles(const DUnit*, const int32_t*, int2*);
 
 // decode.hip
 __global__ void k_dec_count_chunks(const uint8_t*, const int64_t*, const int64_t*, int32_t, int32_t*, uint32_t*);

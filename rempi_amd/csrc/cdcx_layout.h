@@ -99,6 +99,24 @@ struct SortTile {
   int32_t tile;
 };
 
+// Totals of a batch that the host reads back to size buffers and grids (lists.hip).
+struct EncTotals {
+  int32_t n_units;       // non-empty (chunk, table) pairs
+  int32_t n_sort_tiles;  // sum of ceil(M / kSortTile)
+  int32_t n_fail;        // units the windowed rank could not rank
+  int32_t n_big;         // units with more epoch sources than the small k_epoch instance holds
+  int64_t n_segs;        // closed-prefix segments
+  int64_t matched, with_next, runs, sources;  // sums of M, W, U, S
+  int64_t w1n;           // sum of n + 1 (lane-tier leaf scratch rows)
+};
+struct DecTotals {
+  int64_t n_units;
+  int64_t rows;       // sum of M + 1 (decoder scratch rows)
+  int64_t records;    // reconstructed records
+  int64_t keys;       // sum of M
+  int64_t rec_tiles;  // k_dec_records tiles
+};
+
 struct DChunk {
   int64_t off;  // absolute payload offset in the input buffer
   int64_t len;

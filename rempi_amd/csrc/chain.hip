@@ -474,6 +474,7 @@ __global__ void __launch_bounds__(64) k_chain_entries(Unit* __restrict__ units, 
     K += sg.lmax;
     if (s > 0) j = qexit[u.a + sg.start + j];
   }
+  K = min(K, u.M);  // (always true for a valid permutation; keeps the output layout inside its bound)
   u.K = K;
   u.P = u.M - K;
 }

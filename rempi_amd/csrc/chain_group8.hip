@@ -65,7 +65,28 @@ __device__ __forceinline__ int32_t ldg(const int32_t* base, uint32_t boff) {
 __device__ __forceinline__ void stg(int32_t* base, uint32_t boff, int32_t v) {
   *reinterpret_cast<int32_t*>(reinterpret_cast<char*>(base) + boff) = v;
 }
+#ifdef CDCX_CHAIN_STATS
+// Wave-level path counts (profiling build only): the first active lane of the wave counts.
+__device__ unsigned long long g8_stats[24];
+#define G8_STAT(n)                                                                               \
+  do {                                                                                           \
+    if ((int)(threadIdx.x & 63) == __ffsll((long long)__builtin_amdgcn_ballot_w64(true)) - 1) st[n]++; \
+  } while (0)
+#else
+#define G8_STAT(n) do { } while (0)
+#endif
 }  // namespace
+
+#ifdef CDCX_CHAIN_STATS
+extern "C" int cdcx_debug_g8_stats(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g8_stats), sizeof(g8_stats)) != hipSuccess) return 1;
+  if (reset) {
+    unsigned long long z[24] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g8_stats), z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
 
 __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ units, Seg* __restrict__ segs,
                                                     const int32_t* __restrict__ list, const int32_t* __restrict__ nlist_p,
@@ -100,6 +121,9 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
   int32_t top = 0, cw0 = 0, cw1 = 0, pval = 0, rj = j;
   // wave-uniform phase: every group's row i sits at slot t of its frame
   int t = 0;
+#ifdef CDCX_CHAIN_STATS
+  unsigned long long st[24] = {};
+#endif
 
   auto ring_par = [&](int32_t x) -> int32_t {  // parent of row x < i of this segment
     int32_t p = ring[x & (R - 1)].x;
@@ -115,6 +139,7 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
   };
 
   while (true) {
+    G8_STAT(0);
     if (t == G) {  // every group at once: store the frame's parents, slide the windows
       t = 0;
       if (rj >= s0) stg(par, ab + 4u * (uint32_t)rj, pval);  // (rows before s0: the previous segment's, stored there)
@@ -129,6 +154,7 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
         __builtin_amdgcn_s_setprio(0);
     }
     if (i >= s1) {
+      G8_STAT(1);
       if (si >= 0) {
         if (j < t && rj >= s0) stg(par, ab + 4u * (uint32_t)rj, pval);
         if (j == 0) {
@@ -141,6 +167,7 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
       k = first8(k);
       const int64_t kk = (int64_t)blockIdx.x + (int64_t)gridDim.x * k;
       if (kk >= nlist) break;
+      G8_STAT(20);
       si = list[kk];
       const Seg sg = segs[si];
       ab = (uint32_t)units[sg.unit].a << 2;
@@ -160,13 +187,20 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
     const int32_t c = cv & 0x7fffffff;
     // does any group of this wave use its B slots in this iteration?
     const bool useB = m_gt(nl, G) != 0;
+    G8_STAT(2);
+    if (useB) G8_STAT(3);
+#ifdef CDCX_CHAIN_STATS
+    st[21] += __popcll(__builtin_amdgcn_ballot_w64(true));
+#endif
 
     // ---- k*: highest level whose top column is smaller than c ---------------------------
     const uint32_t tm = grp8(m_lt(j, lmax) & m_lt(top, c), sh);
     int32_t ks = tm ? lmax - (__ffs(tm) - 1) : 0;
     if (tm == 0 && lmax > G) {  // below the register tops: binary search the spilled levels
       int32_t lo = 1, hi = lmax - G;
+      G8_STAT(4);
       while (lo <= hi) {
+        G8_STAT(5);
         const int32_t mid = (lo + hi) >> 1;
         if (ldg(topg, tb + 4u * (uint32_t)mid - 4u) < c) {
           ks = mid;
@@ -180,6 +214,7 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
     // ---- parent --------------------------------------------------------------------------
     int32_t pv, pslot = 2 * G;  // pslot: the adopted leaf's slot, 16 = none
     if (ks >= 1) {
+      G8_STAT(6);
       const mask64 jn = m_lt(j, nl);
       uint32_t eq = grp8(jn & m_eq(llv, ks) & m_lt(lcol, c), sh);
       uint32_t gt = grp8(jn & m_gt(llv, ks), sh);
@@ -194,12 +229,16 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
       int32_t anc = -1;
       bool interior = false;
       if (need) {
+        G8_STAT(7);
         // every slot before wa holding a deeper leaf climbs to its level-k* ancestor at once
         const bool mine = (need >> j) & 1u;
         int32_t x = lid, col = 0x7fffffff;
         if (mine) {
 #pragma unroll 1
-          for (int32_t d = llv - ks; d > 0; d--) x = ring_par(x);
+          for (int32_t d = llv - ks; d > 0; d--) {
+            G8_STAT(8);
+            x = ring_par(x);
+          }
           col = ring_col(x);
         }
         uint32_t ok = grp8(m_lt(col, c), sh);
@@ -215,6 +254,7 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
           ok |= grp8(m_lt(colB, c), sh) << G;
         }
         if (ok) {
+          G8_STAT(9);
           win = __ffs(ok) - 1;
           interior = true;
           const int32_t ad = bp4 + ((win & 7) << 2);
@@ -241,10 +281,12 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
         pslot = win;
       }
     } else if (ord == 0) {
+      G8_STAT(10);
       pv = -1;  // first segment: level 1 hangs off the root
     } else {
       // outside parent, resolved at stitching from (ordinal, first leaf) -- chain.hip
       pv = -2 - nrel1;
+      G8_STAT(11);
       const int32_t f = first8(lid);
       if (j == 0) stg(exta, ab + 4u * (uint32_t)i, nl > 0 ? f : -1);
       nrel1++;
@@ -255,12 +297,15 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
     // ---- tops ------------------------------------------------------------------------------
     const int32_t k = ks + 1;
     const bool grow = k > lmax;
+    if (grow && lmax >= G) G8_STAT(12);
+    if (!grow && lmax - k >= G) G8_STAT(13);
     if (grow && j == G - 1 && lmax >= G) stg(topg, tb + 4u * (uint32_t)lmax - 4u * G, top);
     if (!grow && lmax - k >= G && j == 0) stg(topg, tb + 4u * (uint32_t)k - 4u, c);
     const int32_t tshift = prev8(top);
     top = grow ? ((j == 0) ? c : tshift) : ((j == lmax - k) ? c : top);
     qcnt = grow ? 0 : qcnt;
     lmax = grow ? k : lmax;
+    if (k == lmax) G8_STAT(14);
     if (k == lmax && j == 0) stg(qn, tb + 4u * (uint32_t)qcnt, i);
     qcnt += (k == lmax) ? 1 : 0;
 
@@ -289,9 +334,11 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
     }
     // (the sweep comes before the append: the new node, on the open column itself, is never swept)
     if (cv < 0) {
+      G8_STAT(15);
       uint32_t dead = grp8(m_lt(j, nl) & m_lt(lcol, c), sh);
       if (!useB) {
         if (dead) {
+          G8_STAT(16);
           const bool alive = j < nl && !((dead >> j) & 1u);
           const int32_t dst = alive ? j - __popc(dead & below(j)) : G - 1;
           const int32_t ad = bp4 + (dst << 2);
@@ -303,6 +350,7 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
       } else {
         dead |= grp8(m_lt(j + G, nl) & m_lt(lcolB, c), sh) << G;
         if (dead) {
+          G8_STAT(17);
           // compaction through LDS: slot s (alive) lands at s - #dead below it
           const bool aliveA = j < nl && !((dead >> j) & 1u), aliveB = j + G < nl && !((dead >> (j + G)) & 1u);
           if (aliveA) {
@@ -331,6 +379,7 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
     }
     if (useB) {
       if (nl == 2 * G) {  // leaf list outgrows the group: hand the segment to the next tier
+        G8_STAT(18);
         if (j == 0) ovf[atomicAdd(novf, 1)] = si;
         si = -1;
         s1 = i + 1;  // the rest of this iteration runs on junk state and ends the segment
@@ -357,6 +406,10 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
     i++;
     t++;
   }
+#ifdef CDCX_CHAIN_STATS
+  for (int q = 0; q < 24; q++)
+    if (st[q]) atomicAdd(&g8_stats[q], st[q]);
+#endif
 }
 
 }  // namespace cdcx

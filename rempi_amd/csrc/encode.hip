@@ -287,18 +287,23 @@ __global__ void __launch_bounds__(64) k_chunks(const int32_t* __restrict__ rec, 
   if (l == 0) nchunks[r] = k;
 }
 
-// For every (chunk, table): the table's T-order sub-range that falls inside the chunk.
-__global__ void __launch_bounds__(256) k_units_lb(const Chunk* __restrict__ ch, int32_t n_chunks,
-                                                  const int64_t* __restrict__ lb_off, const int32_t* __restrict__ nsets,
-                                                  const int32_t* __restrict__ tstart, const int64_t* __restrict__ rec_off,
-                                                  const int32_t* __restrict__ t2s, int2* __restrict__ lohi) {
+// For every (chunk, table): the table's T-order sub-range that falls inside the chunk; per
+// chunk the number of non-empty tables (its units) and the sum of their lengths + 1.
+__global__ void __launch_bounds__(kMaxSets) k_units_lb(const Chunk* __restrict__ ch, int32_t n_chunks,
+                                                       const int64_t* __restrict__ lb_off, const int32_t* __restrict__ nsets,
+                                                       const int32_t* __restrict__ tstart, const int64_t* __restrict__ rec_off,
+                                                       const int32_t* __restrict__ t2s, int2* __restrict__ lohi,
+                                                       int32_t* __restrict__ ucnt, int64_t* __restrict__ uw) {
+  __shared__ int64_t lds[kMaxSets / kWave];
   const int c = blockIdx.x;
   if (c >= n_chunks) return;
   const Chunk C = ch[c];
   const int T = nsets[C.rank];
   const int64_t rb = rec_off[C.rank];
   const int32_t* ts = tstart + C.rank * (kMaxSets + 1);
-  for (int tb = threadIdx.x; tb < T; tb += blockDim.x) {
+  const int tb = threadIdx.x;
+  int64_t mine = 0;
+  if (tb < T) {
     int32_t r0 = ts[tb], r1 = ts[tb + 1];
     auto lb = [&](int32_t x) {
       int32_t lo = r0, hi = r1;
@@ -308,7 +313,14 @@ __global__ void __launch_bounds__(256) k_units_lb(const Chunk* __restrict__ ch, 
       }
       return lo;
     };
-    lohi[lb_off[c] + tb] = make_int2(lb(C.s), lb(C.e + 1));
+    const int2 lh = make_int2(lb(C.s), lb(C.e + 1));
+    lohi[lb_off[c] + tb] = lh;
+    if (lh.y > lh.x) mine = ((int64_t)1 << 40) + (lh.y - lh.x) + 1;
+  }
+  const int64_t tot = block_sum<kMaxSets>(mine, lds);
+  if (threadIdx.x == 0) {
+    ucnt[c] = (int32_t)(tot >> 40);
+    uw[c] = tot & (((int64_t)1 << 40) - 1);
   }
 }
 
@@ -394,6 +406,7 @@ __global__ void __launch_bounds__(256) k_window_rank(Unit* __restrict__ units, c
   __shared__ uint64_t xk[NX + NX / 4 + 1];
   __shared__ int32_t rk[kSortTile];
   const SortTile w = st[blockIdx.x];
+  if (w.unit < 0) return;  // past the batch's sort tiles (the grid is an upper bound)
   const Unit u = units[w.unit];
   const int32_t t0 = w.tile * kSortTile;
   const int len = min(kSortTile, u.M - t0);
