@@ -30,7 +30,7 @@ using namespace cdcx;
 namespace {
 
 enum KernelId {
-  K_SET_PRESENCE, K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_INC0, K_TILE_SUM, K_RANK_SCAN, K_TILE_P0,
+  K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_RANK_SCAN,
   K_CHUNKS, K_UNITS_LB, K_LISTS, K_UNIT_PREP, K_WINDOW_RANK, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_G8, K_CHAIN_G16, K_CHAIN_G64, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
   K_WRITE_UNITS, K_CHUNK_HEADERS, K_FOOTER_ORDER, K_FOOTER_WRITE, K_WRITE_KEYS,
   K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS, K_DEC_PACK, K_VERIFY,
@@ -38,8 +38,8 @@ enum KernelId {
   K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
-  "k_set_presence", "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_inc0", "k_tile_sum", "k_rank_scan",
-  "k_tile_p0", "k_chunks", "k_units_lb", "k_lists", "k_unit_prep", "k_window_rank", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp8", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
+  "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_rank_scan",
+  "k_chunks", "k_units_lb", "k_lists", "k_unit_prep", "k_window_rank", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp8", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
   "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records", "k_dec_pack_tables", "k_verify_roundtrip",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
@@ -401,14 +401,13 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   uint32_t* d_hist = c->buf<uint32_t>("hist", NT * kMaxSets);
   int32_t* d_base = c->buf<int32_t>("base", NT * kMaxSets);
   int32_t* d_tstart = c->buf<int32_t>("tstart", (size_t)R * (kMaxSets + 1));
-  uint8_t* d_tfirst = c->buf<uint8_t>("tfirst", N);
-  HIPCHK(hipMemsetAsync(d_tfirst, 0, N, s));
+  uint8_t* d_prevm = c->buf<uint8_t>("prevm", NT * kMaxSets);
   TRec* d_trec = c->buf<TRec>("trec", N);
   int32_t* d_t2s = c->buf<int32_t>("t2s", N);
-  uint8_t* d_inc0 = c->buf<uint8_t>("inc0s", N);
+  uint8_t* d_inc0 = c->buf<uint8_t>("inc0s", NT * kTile);  // per tile: a rank's flags start kTile-aligned
   int32_t* d_tsum = c->buf<int32_t>("tsum", NT);
   int32_t* d_toff = c->buf<int32_t>("toff", NT);
-  int32_t* d_p0 = c->buf<int32_t>("p0", N + R);
+  int32_t* d_rtot = c->buf<int32_t>("rtot", R);
   std::vector<int64_t> ccap_off(R + 1, 0);
   for (int r = 0; r < R; r++) ccap_off[r + 1] = ccap_off[r] + nrec[r] / (maxl + 1 > 0 ? maxl + 1 : 1) + 2;
   int64_t* d_ccap = c->upload("ccap_off", ccap_off, s);
@@ -418,20 +417,16 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   c->launch(K_TILE_HIST, k_tile_hist, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, d_hist, d_presence, d_err);
   c->launch(K_SET_DENSE, k_set_dense, dim3(R), dim3(kMaxSets), s, (const uint32_t*)d_presence, d_dense, d_setlist, d_nsets);
   c->launch(K_HIST_SCAN, k_hist_scan, dim3(R), dim3(256), s, (const uint32_t*)d_hist, (const int32_t*)d_tile0,
-            (const int32_t*)d_ntiles, (const int32_t*)d_nsets, (const int32_t*)d_setlist, (const int64_t*)d_rec_off, d_base,
-            d_tstart, d_tfirst);
-  int32_t* d_s2t = c->buf<int32_t>("lrank", N);  // stream -> T-order; dead before the tile sort needs "lrank"
+            (const int32_t*)d_ntiles, (const int32_t*)d_nsets, (const int32_t*)d_setlist, d_base, d_tstart, d_prevm);
+  // (the scatter also forms the records' length increments and their tile sums)
   c->launch(K_SCATTER, k_scatter, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, (const int16_t*)d_dense,
-            (const int32_t*)d_base, (const int64_t*)d_rec_off, d_trec, d_t2s, d_s2t);
-  c->launch(K_INC0, k_inc0, dim3(NT), dim3(256), s, (const TRec*)d_trec, (const int32_t*)d_s2t, (const uint8_t*)d_tfirst,
-            (const Tile*)d_tiles, (const int64_t*)d_rec_off, d_inc0, d_tsum);
+            (const int32_t*)d_base, (const uint8_t*)d_prevm, (const int64_t*)d_rec_off, d_trec, d_t2s, d_inc0, d_tsum);
   c->launch(K_RANK_SCAN, k_rank_scan, dim3(R), dim3(256), s, (const int32_t*)d_tsum, (const int32_t*)d_tile0,
-            (const int32_t*)d_ntiles, d_toff);
-  c->launch(K_TILE_P0, k_tile_p0, dim3(NT), dim3(256), s, (const uint8_t*)d_inc0, (const Tile*)d_tiles,
-            (const int32_t*)d_toff, (const int64_t*)d_rec_off, (const int64_t*)d_nrec, d_p0);
+            (const int32_t*)d_ntiles, d_toff, d_rtot);
   c->launch(K_CHUNKS, k_chunks, dim3(R), dim3(64), s, d_rec, (const int64_t*)d_rec_off, (const int64_t*)d_nrec,
-            (const int32_t*)d_p0, (const uint8_t*)d_inc0, (const int32_t*)d_t2s, (const int32_t*)d_tstart,
-            (const int32_t*)d_nsets, (const int64_t*)d_ccap, maxl, d_chunk_cap, d_nchunks);
+            (const int32_t*)d_toff, (const int32_t*)d_rtot, (const int32_t*)d_tile0, (const uint8_t*)d_inc0,
+            (const int32_t*)d_t2s, (const int32_t*)d_tstart, (const int32_t*)d_nsets, (const int64_t*)d_ccap, maxl,
+            d_chunk_cap, d_nchunks);
 
   // Wait 1: tables and chunks per rank -> number of chunks and of (chunk, table) slots.
   std::vector<int32_t> cbase(R + 1, 0);

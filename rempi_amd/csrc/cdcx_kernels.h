@@ -21,15 +21,14 @@ struct GenArgs {
 // encode.hip
 __global__ void k_set_dense(const uint32_t*, int16_t*, int32_t*, int32_t*);
 __global__ void k_tile_hist(const int32_t*, const Tile*, uint32_t*, uint32_t*, uint32_t*);
-__global__ void k_hist_scan(const uint32_t*, const int32_t*, const int32_t*, const int32_t*, const int32_t*,
-                            const int64_t*, int32_t*, int32_t*, uint8_t*);
-__global__ void k_scatter(const int32_t*, const Tile*, const int16_t*, const int32_t*, const int64_t*, TRec*, int32_t*,
-                          int32_t*);
-__global__ void k_inc0(const TRec*, const int32_t*, const uint8_t*, const Tile*, const int64_t*, uint8_t*, int32_t*);
-__global__ void k_rank_scan(const int32_t*, const int32_t*, const int32_t*, int32_t*);
-__global__ void k_tile_p0(const uint8_t*, const Tile*, const int32_t*, const int64_t*, const int64_t*, int32_t*);
-__global__ void k_chunks(const int32_t*, const int64_t*, const int64_t*, const int32_t*, const uint8_t*, const int32_t*,
-                         const int32_t*, const int32_t*, const int64_t*, int64_t, int2*, int32_t*);
+__global__ void k_hist_scan(const uint32_t*, const int32_t*, const int32_t*, const int32_t*, const int32_t*, int32_t*,
+                            int32_t*, uint8_t*);
+__global__ void k_scatter(const int32_t*, const Tile*, const int16_t*, const int32_t*, const uint8_t*, const int64_t*,
+                          TRec*, int32_t*, uint8_t*, int32_t*);
+__global__ void k_rank_scan(const int32_t*, const int32_t*, const int32_t*, int32_t*, int32_t*);
+__global__ void k_chunks(const int32_t*, const int64_t*, const int64_t*, const int32_t*, const int32_t*, const int32_t*,
+                         const uint8_t*, const int32_t*, const int32_t*, const int32_t*, const int64_t*, int64_t, int2*,
+                         int32_t*);
 __global__ void k_units_lb(const Chunk*, int32_t, const int64_t*, const int32_t*, const int32_t*, const int64_t*,
                            const int32_t*, int2*, int32_t*, int64_t*);
 __global__ void k_unit_prep(Unit*, const TRec*, uint64_t*, int32_t*, int32_t*, int32_t*, uint64_t*, uint32_t*);

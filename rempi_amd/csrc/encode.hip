@@ -18,22 +18,30 @@ namespace cdcx {
 
 // ---------------------------------------------------------------------------------------
 // Set discovery + per-tile histograms in one pass over the records: hist[tile][set id]
-// and, per rank, which matching_set_ids occur (limit: [0, kMaxSets)).
+// (bit 31: the tile's last record of that set is a matched event -- what the first record of
+// the set in a later tile needs to know to tell whether it starts a new unmatched run) and,
+// per rank, which matching_set_ids occur (limit: [0, kMaxSets)).
 __global__ void __launch_bounds__(256) k_tile_hist(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
                                                    uint32_t* __restrict__ hist, uint32_t* __restrict__ presence,
                                                    uint32_t* err) {
   __shared__ uint32_t h[kMaxSets];
+  __shared__ uint32_t last[kMaxSets];  // max over the set's records of (index in tile + 1) << 1 | matched
   h[threadIdx.x] = 0;
+  last[threadIdx.x] = 0;
   __syncthreads();
   const Tile t = tiles[blockIdx.x];
   for (int i = threadIdx.x; i < t.len; i += blockDim.x) {
-    const int32_t sid = rec[(t.start + i) * 8 + 7];
+    const int32_t* rp = rec + (t.start + i) * 8;
+    const int32_t sid = rp[7];
     if ((uint32_t)sid >= (uint32_t)kMaxSets) raise_error(err, kErrLimit);
-    else atomicAdd(&h[sid], 1u);
+    else {
+      atomicAdd(&h[sid], 1u);
+      atomicMax(&last[sid], ((uint32_t)(i + 1) << 1) | (rp[2] == 1 ? 1u : 0u));
+    }
   }
   __syncthreads();
   const uint32_t v = h[threadIdx.x];
-  hist[(int64_t)blockIdx.x * kMaxSets + threadIdx.x] = v;
+  hist[(int64_t)blockIdx.x * kMaxSets + threadIdx.x] = v | ((last[threadIdx.x] & 1u) << 31);
   const uint64_t nz = __builtin_amdgcn_ballot_w64(v != 0);
   if (lane_id() == 0 && (uint32_t)nz) atomicOr(&presence[t.rank * (kMaxSets / 32) + wave_id() * 2], (uint32_t)nz);
   if (lane_id() == 32 && (uint32_t)(nz >> 32)) atomicOr(&presence[t.rank * (kMaxSets / 32) + wave_id() * 2 + 1], (uint32_t)(nz >> 32));
@@ -55,29 +63,35 @@ __global__ void __launch_bounds__(kMaxSets) k_set_dense(const uint32_t* __restri
 }
 
 // Per rank: exclusive scan of the tile histograms in (table, tile) order -> where each
-// tile's records of each table start in T-order; table starts; first-of-table flags.
+// tile's records of each table start in T-order; table starts; and for every (tile, table)
+// what the table's last record before the tile was: prevm = 0 none, 1 unmatched, 3 matched.
 __global__ void __launch_bounds__(256) k_hist_scan(const uint32_t* __restrict__ hist, const int32_t* __restrict__ tile0,
                                                    const int32_t* __restrict__ ntiles, const int32_t* __restrict__ nsets,
-                                                   const int32_t* __restrict__ setlist, const int64_t* __restrict__ rec_off,
-                                                   int32_t* __restrict__ base, int32_t* __restrict__ tstart,
-                                                   uint8_t* __restrict__ tfirst) {
+                                                   const int32_t* __restrict__ setlist, int32_t* __restrict__ base,
+                                                   int32_t* __restrict__ tstart, uint8_t* __restrict__ prevm) {
   __shared__ int32_t lds[4];
   const int r = blockIdx.x;
   const int T = nsets[r], t0 = tile0[r], nt = ntiles[r];
   int32_t run = 0;
   for (int t = 0; t < T; t++) {
     const int sid = setlist[r * kMaxSets + t];
-    if (threadIdx.x == 0) {
-      tstart[r * (kMaxSets + 1) + t] = run;
-      tfirst[rec_off[r] + run] = 1;
-    }
+    if (threadIdx.x == 0) tstart[r * (kMaxSets + 1) + t] = run;
+    int32_t carry = 0;  // (tile + 1) << 2 | flags of the table's latest non-empty tile so far
     for (int c = 0; c < nt; c += 256) {
       int i = c + threadIdx.x;
-      int32_t v = (i < nt) ? (int32_t)hist[(int64_t)(t0 + i) * kMaxSets + sid] : 0;
+      const uint32_t hv = (i < nt) ? hist[(int64_t)(t0 + i) * kMaxSets + sid] : 0u;
+      const int32_t v = (int32_t)(hv & 0x7fffffffu);
       int32_t tot;
       int32_t ex = block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);
-      if (i < nt) base[(int64_t)(t0 + i) * kMaxSets + t] = run + ex;
+      const int32_t f = v ? (((i + 1) << 2) | 1 | (int32_t)((hv >> 31) << 1)) : 0;
+      int32_t ftot;
+      const int32_t fex = max(carry, block_exclusive_scan<256>(f, 0, OpMax(), lds, &ftot));
+      if (i < nt) {
+        base[(int64_t)(t0 + i) * kMaxSets + t] = run + ex;
+        prevm[(int64_t)(t0 + i) * kMaxSets + t] = (uint8_t)(fex & 3);
+      }
       run += tot;
+      carry = max(carry, ftot);
     }
   }
   if (threadIdx.x == 0) tstart[r * (kMaxSets + 1) + T] = run;
@@ -86,12 +100,22 @@ __global__ void __launch_bounds__(256) k_hist_scan(const uint32_t* __restrict__ 
 // Stable scatter of records into T-order.  Rounds of 256 consecutive records; within a
 // wave, records with the same table find each other with 8 ballots (one per bit of the
 // table index), which keeps the partition stable for any number of tables.
+//
+// The same pass forms inc0, the length increment of each record if chunks were infinite
+// (add(), :189-212): 1 for a matched event, 1 for an unmatched event that starts a new run of
+// its table (the table's previous record is a matched event, or there is none), else 0.  The
+// previous record of the table is a lower lane of the wave, or the last one of an earlier
+// (round, wave) slot of the tile (carried through the slot scan), or the last one before the
+// tile (prevm).  inc0s is laid out per tile (tile * kTile + index), so a rank's flags are
+// contiguous from a kTile-aligned start; tsum = the tile's sum.
 __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
                                                  const int16_t* __restrict__ dense, const int32_t* __restrict__ base,
-                                                 const int64_t* __restrict__ rec_off, TRec* __restrict__ trec,
-                                                 int32_t* __restrict__ t2s, int32_t* __restrict__ s2t) {
+                                                 const uint8_t* __restrict__ prevm, const int64_t* __restrict__ rec_off,
+                                                 TRec* __restrict__ trec, int32_t* __restrict__ t2s,
+                                                 uint8_t* __restrict__ inc0s, int32_t* __restrict__ tsum) {
   constexpr int ROUNDS = kTile / 256;
-  __shared__ int32_t wc[ROUNDS * 4 * kMaxSets];  // [round][wave][table]
+  __shared__ int32_t wc[ROUNDS * 4 * kMaxSets];  // [round][wave][table]: count | last record's flags << 16
+  __shared__ int32_t lds[4];
   for (int i = threadIdx.x; i < ROUNDS * 4 * kMaxSets; i += 256) wc[i] = 0;
   const Tile t = tiles[blockIdx.x];
   const int w = wave_id(), l = lane_id();
@@ -112,6 +136,7 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
   __syncthreads();
   int my_t[ROUNDS];
   int my_rank[ROUNDS];
+  int my_prev[ROUNDS];  // flags of the table's previous record when it is a lower lane of this wave, else 0
 #pragma unroll
   for (int j = 0; j < ROUNDS; j++) {
     const int i = j * 256 + threadIdx.x;
@@ -124,29 +149,38 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
       uint64_t m = __builtin_amdgcn_ballot_w64(((tb >> b) & 1) != 0);
       peers &= ((tb >> b) & 1) ? m : ~m;
     }
+    const uint64_t mm = __builtin_amdgcn_ballot_w64(valid && lo[j].z == 1);
+    const uint64_t lower = peers & lt_mask;
     my_t[j] = tb;
-    my_rank[j] = __popcll(peers & lt_mask);
-    if (valid && __popcll(peers & lt_mask) == 0) wc[(j * 4 + w) * kMaxSets + tb] = __popcll(peers);
+    my_rank[j] = __popcll(lower);
+    my_prev[j] = lower ? (1 | (int)(((mm >> (63 - __clzll((long long)lower))) & 1) << 1)) : 0;
+    if (valid && lower == 0)
+      wc[(j * 4 + w) * kMaxSets + tb] =
+          __popcll(peers) | ((1 | (int)(((mm >> (63 - __clzll((long long)peers))) & 1) << 1)) << 16);
   }
   __syncthreads();
   {  // exclusive scan over (round, wave) for each table: thread = table
     const int tb = threadIdx.x;
     int32_t run = 0;
+    int32_t pf = prevm[(int64_t)blockIdx.x * kMaxSets + tb];
     for (int k = 0; k < ROUNDS * 4; k++) {
-      int32_t v = wc[k * kMaxSets + tb];
-      wc[k * kMaxSets + tb] = run;
-      run += v;
+      const int32_t v = wc[k * kMaxSets + tb];
+      wc[k * kMaxSets + tb] = run | (pf << 16);
+      run += v & 0xffff;
+      if (v >> 16) pf = v >> 16;
     }
   }
   __syncthreads();
   const int64_t rb = rec_off[t.rank];
   const int32_t spos0 = (int32_t)(t.start - rb);
+  int32_t sum = 0;
 #pragma unroll
   for (int j = 0; j < ROUNDS; j++) {
     const int i = j * 256 + threadIdx.x;
     if (i >= t.len) continue;
     const int tb = my_t[j];
-    const int32_t pos = base[(int64_t)blockIdx.x * kMaxSets + tb] + wc[(j * 4 + w) * kMaxSets + tb] + my_rank[j];
+    const int32_t slot = wc[(j * 4 + w) * kMaxSets + tb];
+    const int32_t pos = base[(int64_t)blockIdx.x * kMaxSets + tb] + (slot & 0xffff) + my_rank[j];
     // lo = {count, type, flag, rank}, hi = {with_next, index, clock, set}
     TRec o;
     const bool matched = (lo[j].z == 1);
@@ -156,36 +190,19 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
     o.info = matched ? (0x80000000u | (hi[j].x != 0 ? 1u : 0u)) : 0u;
     trec[rb + pos] = o;
     t2s[rb + pos] = spos0 + i;
-    s2t[t.start + i] = pos;
-  }
-}
-
-// inc0: length increment of each record if chunks were infinite (add(), :189-212): 1 for a
-// matched event, 1 for an unmatched event that starts a new run of its table, else 0.
-// Walked in stream order (the T-order position comes from s2t), so the flags are written
-// coalesced and the T-order reads advance sequentially per table; the tile's sum is formed
-// here too.
-__global__ void __launch_bounds__(256) k_inc0(const TRec* __restrict__ trec, const int32_t* __restrict__ s2t,
-                                              const uint8_t* __restrict__ tfirst, const Tile* __restrict__ tiles,
-                                              const int64_t* __restrict__ rec_off, uint8_t* __restrict__ inc0s,
-                                              int32_t* __restrict__ tsum) {
-  __shared__ int32_t lds[4];
-  const Tile t = tiles[blockIdx.x];
-  const int64_t rb = rec_off[t.rank];
-  int32_t sum = 0;
-  for (int i = threadIdx.x; i < t.len; i += blockDim.x) {
-    const int64_t g = rb + s2t[t.start + i];
-    uint8_t inc = 1;
-    if (!(trec[g].info >> 31) && !tfirst[g] && !(trec[g - 1].info >> 31)) inc = 0;
-    inc0s[t.start + i] = inc;
+    const int prev = my_prev[j] ? my_prev[j] : (slot >> 16);
+    const int32_t inc = (matched || prev != 1) ? 1 : 0;
+    inc0s[(int64_t)blockIdx.x * kTile + i] = (uint8_t)inc;
     sum += inc;
   }
   sum = block_sum<256>(sum, lds);
   if (threadIdx.x == 0) tsum[blockIdx.x] = sum;
 }
 
+// Per rank: exclusive scan of the tile sums of inc0 (toff) and their total (rtot).
 __global__ void __launch_bounds__(256) k_rank_scan(const int32_t* __restrict__ tsum, const int32_t* __restrict__ tile0,
-                                                   const int32_t* __restrict__ ntiles, int32_t* __restrict__ toff) {
+                                                   const int32_t* __restrict__ ntiles, int32_t* __restrict__ toff,
+                                                   int32_t* __restrict__ rtot) {
   __shared__ int32_t lds[4];
   const int r = blockIdx.x;
   const int t0 = tile0[r], nt = ntiles[r];
@@ -197,51 +214,56 @@ __global__ void __launch_bounds__(256) k_rank_scan(const int32_t* __restrict__ t
     if (i < nt) toff[t0 + i] = run + ex;
     run += tot;
   }
-}
-
-// p0[r][i] = sum of inc0 over stream positions < i (n_r + 1 entries per rank).
-__global__ void __launch_bounds__(256) k_tile_p0(const uint8_t* __restrict__ inc0s, const Tile* __restrict__ tiles,
-                                                 const int32_t* __restrict__ toff, const int64_t* __restrict__ rec_off,
-                                                 const int64_t* __restrict__ nrec, int32_t* __restrict__ p0) {
-  __shared__ int32_t lds[4];
-  const Tile t = tiles[blockIdx.x];
-  const int64_t p0b = rec_off[t.rank] + t.rank;
-  const int64_t spos = t.start - rec_off[t.rank];
-  constexpr int PER = kTile / 256;
-  int32_t v[PER], s = 0;
-#pragma unroll
-  for (int j = 0; j < PER; j++) {
-    int i = threadIdx.x * PER + j;
-    v[j] = (i < t.len) ? inc0s[t.start + i] : 0;
-    s += v[j];
-  }
-  int32_t tot;
-  int32_t ex = block_exclusive_scan<256>(s, 0, OpAdd(), lds, &tot) + toff[blockIdx.x];
-#pragma unroll
-  for (int j = 0; j < PER; j++) {
-    int i = threadIdx.x * PER + j;
-    if (i < t.len) p0[p0b + spos + i] = ex;
-    ex += v[j];
-  }
-  if (spos + t.len == nrec[t.rank] && threadIdx.x == 255) p0[p0b + spos + t.len] = ex;
+  if (threadIdx.x == 0) rtot[r] = run;
 }
 
 // Chunk boundaries, one wave per rank (extract_encoder_input_format_chunk, :740-778):
 // a chunk starting at s ends at the first e with L(s,e) > REMPI_MAX and with_next(e) == 0,
-// or at the end of the stream.  L(s,e) = p0[e+1]-p0[s] + #tables whose first record in
-// [s,e] is an unmatched run continuation (inc0 == 0; inside the chunk it starts a run).
+// or at the end of the stream.  L(s,e) = p0(e+1)-p0(s) + #tables whose first record in
+// [s,e] is an unmatched run continuation (inc0 == 0; inside the chunk it starts a run),
+// p0(x) = sum of inc0 over stream positions < x.
+//
+// p0 is never materialised: at a tile boundary it is the tile offset (toff), inside a tile
+// the wave adds the flags before x (16 bytes per lane).  The search for e first walks tile
+// boundaries (tile offsets only), then the one tile that holds the crossing, from registers.
 __global__ void __launch_bounds__(64) k_chunks(const int32_t* __restrict__ rec, const int64_t* __restrict__ rec_off,
-                                               const int64_t* __restrict__ nrec, const int32_t* __restrict__ p0,
+                                               const int64_t* __restrict__ nrec, const int32_t* __restrict__ toff,
+                                               const int32_t* __restrict__ rtot, const int32_t* __restrict__ tile0,
                                                const uint8_t* __restrict__ inc0s, const int32_t* __restrict__ t2s,
                                                const int32_t* __restrict__ tstart, const int32_t* __restrict__ nsets,
                                                const int64_t* __restrict__ ccap_off, int64_t max_len,
                                                int2* __restrict__ chunks, int32_t* __restrict__ nchunks) {
   const int r = blockIdx.x, l = lane_id();
-  const int64_t rb = rec_off[r], p0b = rb + r;
+  const int64_t rb = rec_off[r];
   const int32_t n = (int32_t)nrec[r];
+  const int32_t t0 = tile0[r], nt = (n + kTile - 1) / kTile;
   const int T = nsets[r];
   const int32_t* ts = tstart + r * (kMaxSets + 1);
-  int32_t s = 0, k = 0;
+  const uint8_t* ib = inc0s + (int64_t)t0 * kTile;  // the rank's flags by stream position
+  const int32_t total = rtot[r];
+  // flags (0/1 bytes) among the first nb of a lane's 16 bytes
+  auto count16 = [](uint4 v, int32_t nb) -> int32_t {
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    int32_t c = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int32_t k = min(max(nb - 4 * q, 0), 4);
+      c += __popc(wv[q] & (k == 4 ? 0xffffffffu : ((1u << (8 * k)) - 1u)));
+    }
+    return c;
+  };
+  auto P = [&](int32_t x) -> int32_t {  // p0(x), 0 <= x <= n
+    const int32_t q = x >> 10, wq = x & (kTile - 1);
+    int32_t v = q < nt ? toff[t0 + q] : total;
+    if (wq) {
+      const int32_t nb = min(max(wq - 16 * l, 0), 16);
+      const int32_t c = nb ? count16(*reinterpret_cast<const uint4*>(ib + (int64_t)q * kTile + 16 * l), nb) : 0;
+      v += wave_reduce(c, OpAdd());
+    }
+    return v;
+  };
+  static_assert(kTile == 1024, "a tile's flags are 16 bytes per lane of one wave");
+  int32_t s = 0, k = 0, p0s = 0;
   while (s < n) {
     int32_t corr[kMaxSets / 64];  // first-in-chunk unmatched continuation positions
 #pragma unroll
@@ -256,33 +278,51 @@ __global__ void __launch_bounds__(64) k_chunks(const int32_t* __restrict__ rec, 
         }
         if (lo < ts[tb + 1]) {
           int32_t f = t2s[rb + lo];
-          if (inc0s[rb + f] == 0) corr[q] = f;
+          if (ib[f] == 0) corr[q] = f;
         }
       }
     }
-    const int32_t p0s = p0[p0b + s];
-    auto L = [&](int32_t e) -> int64_t {
+    auto L = [&](int32_t e, int32_t p_next) -> int64_t {  // p_next = p0(e + 1)
       int c = 0;
 #pragma unroll
       for (int q = 0; q < kMaxSets / 64; q++) c += (corr[q] <= e) ? 1 : 0;
       c = wave_reduce(c, OpAdd());
-      return (int64_t)(p0[p0b + e + 1] - p0s) + c;
+      return (int64_t)(p_next - p0s) + c;
     };
     int32_t e;
-    if (L(n - 1) <= max_len) {
+    if (L(n - 1, total) <= max_len) {
       e = n - 1;
     } else {
-      int32_t lo = s, hi = n - 1;
+      // smallest tile boundary b in ((s >> 10), nt] with L(min(b * kTile, n) - 1) > max_len
+      int32_t lo = (s >> 10) + 1, hi = nt;
       while (lo < hi) {
-        int32_t mid = lo + ((hi - lo) >> 1);
-        if (L(mid) > max_len) hi = mid; else lo = mid + 1;
+        const int32_t mid = (lo + hi) >> 1;  // < nt: the boundary lies inside the stream
+        if (L(mid * kTile - 1, toff[t0 + mid]) > max_len) hi = mid; else lo = mid + 1;
       }
-      e = lo;
+      // the crossing lies in tile lo - 1: its flags, a lane's sum, the sums of the lanes before
+      const int32_t q = lo - 1;
+      const uint4 v = *reinterpret_cast<const uint4*>(ib + (int64_t)q * kTile + 16 * l);
+      const int32_t mine = count16(v, min(max(min(kTile, n - q * kTile) - 16 * l, 0), 16));
+      const int32_t pre = wave_inclusive_scan(mine, OpAdd()) - mine;
+      const int32_t tb0 = toff[t0 + q];
+      auto Pt = [&](int32_t wq) -> int32_t {  // p0(q * kTile + wq), 1 <= wq <= kTile
+        const int32_t ln = __builtin_amdgcn_readfirstlane((wq - 1) >> 4);
+        const uint4 u = make_uint4(__builtin_amdgcn_readlane(v.x, ln), __builtin_amdgcn_readlane(v.y, ln),
+                                   __builtin_amdgcn_readlane(v.z, ln), __builtin_amdgcn_readlane(v.w, ln));
+        return tb0 + __builtin_amdgcn_readlane(pre, ln) + count16(u, wq - 16 * ln);
+      };
+      int32_t xlo = max(s, q * kTile) + 1, xhi = min(lo * kTile, n);  // e + 1 in [xlo, xhi]; L(xhi - 1) > max_len
+      while (xlo < xhi) {
+        const int32_t xm = (xlo + xhi) >> 1;
+        if (L(xm - 1, Pt(xm - q * kTile)) > max_len) xhi = xm; else xlo = xm + 1;
+      }
+      e = xlo - 1;
       while (e < n - 1 && rec[(rb + e) * 8 + 4] != 0) e++;
     }
     if (l == 0) chunks[ccap_off[r] + k] = make_int2(s, e);
     k++;
     s = e + 1;
+    if (s < n) p0s = P(s);
   }
   if (l == 0) nchunks[r] = k;
 }
