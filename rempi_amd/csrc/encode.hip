@@ -991,20 +991,36 @@ __global__ void __launch_bounds__(256) k_pos_cols(const Unit* __restrict__ units
 // list when it moves -- IGNOREs, REMOVEs whose element is still pending (its ADD comes
 // later), ADDs whose element has already moved (its REMOVE came earlier).  Negative when the
 // second occurrence is the REMOVE.  The pair index is a running count of second occurrences.
+//
+// One thread per second occurrence walks its span in an LDS ring of the last 2 K sequence
+// entries.  The ring holds each entry as one signed word q that makes the test two compares:
+// ADD -> partner position (counts when q < s, unsigned), REMOVE -> ~partner (counts when
+// q < -s - 1, i.e. partner > s), IGNORE -> INT32_MIN (always counts).  Spans longer than
+// kLongSpan are left to whole waves afterwards (64 entries per step), so a trace with far
+// moves costs no more than 1/64 of its span per lane.
+namespace {
+__device__ __forceinline__ int32_t delta_word(uint32_t e) {
+  const uint32_t t = e & 3u;
+  const int32_t pt = (int32_t)(e >> 2);
+  return t == kIgn ? INT32_MIN : (t == kAdd ? pt : ~pt);
+}
+}  // namespace
+
 __global__ void __launch_bounds__(256, 8) k_deltas(const Unit* __restrict__ units, const uint32_t* __restrict__ seq,
                                                    const int32_t* __restrict__ sx, int32_t* __restrict__ pid,
                                                    int32_t* __restrict__ pdl) {
-  // LDS and registers are kept small (16 KB, <= 64 VGPRs) so that 8 blocks share a CU: the
-  // kernel waits on LDS and barriers, and occupancy is what hides that.
-  __shared__ int32_t lds[4];
-  __shared__ int2 items[1024];    // second occurrences of the round: {position s, entry}, then {s, delta}
+  // LDS and registers are kept small (<= 20 KB, <= 64 VGPRs) so that 8 blocks share a CU.
   constexpr int32_t RING = 2048;  // the last RING sequence entries, for the span counts
-  __shared__ uint32_t ring[RING];
+  constexpr int32_t kLongSpan = 192;
+  __shared__ int32_t lds[4];
+  __shared__ int2 items[1024];  // second occurrences of the round: {position s, entry}, then {s, delta}
+  __shared__ int32_t ring[RING];
+  __shared__ int32_t longs[1024];  // items of the round with long spans
+  __shared__ int32_t nlong;
   const Unit u = units[blockIdx.x];
   const int64_t a = u.a;
   const uint32_t* sq = seq + 2 * a;
   const int32_t L = 2 * u.P + u.K;
-  const int g = threadIdx.x >> 4, j = threadIdx.x & 15, gw = (threadIdx.x >> 4) & 3;
   const int32_t* sxa = sx + 2 * a;
   int32_t ck = 0;
   // this round's sequence entries; the next round's are loaded while the spans of this one
@@ -1023,9 +1039,10 @@ __global__ void __launch_bounds__(256, 8) k_deltas(const Unit* __restrict__ unit
       if ((e[q] & 3) != kIgn && (int32_t)(e[q] >> 2) < q0 + q) v++;
     int32_t tot;
     int32_t k = block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);
+    if (threadIdx.x == 0) nlong = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      ring[(q0 + q) & (RING - 1)] = e[q];
+      ring[(q0 + q) & (RING - 1)] = delta_word(e[q]);
       if ((e[q] & 3) != kIgn && (int32_t)(e[q] >> 2) < q0 + q) items[k++] = make_int2(q0 + q, (int32_t)e[q]);
     }
     __syncthreads();
@@ -1035,24 +1052,40 @@ __global__ void __launch_bounds__(256, 8) k_deltas(const Unit* __restrict__ unit
       e[q] = (z < L) ? sq[z] : kIgn;
     }
     const int32_t rlo = b + 1024 - RING;  // entries >= rlo are in the ring
-    // one item per 16-lane group: the group counts its span 16 entries at a time
-    for (int32_t it = g; it < tot; it += 16) {
+    for (int32_t it = threadIdx.x; it < tot; it += 256) {
       const int2 item = items[it];
       const int32_t s = item.x, f = (int32_t)((uint32_t)item.y >> 2);
-      int32_t d = 0;
-      for (int32_t z0 = f + 1; z0 < s; z0 += 16) {
-        const int32_t z = z0 + j;
-        uint32_t y = ring[z & (RING - 1)];
-        // entries older than the ring (spans longer than ~1 K) come from memory, behind a
-        // wave-uniform branch so that the common case issues no global load at all
-        if (__builtin_amdgcn_ballot_w64(z < s && z < rlo))
-          if (z < s && z < rlo) y = sq[z];
-        const uint32_t yt = y & 3;
-        const int32_t pt = (int32_t)(y >> 2);
-        const bool c = (z < s) & ((yt == kIgn) | ((yt == kRem) & (pt > s)) | ((yt == kAdd) & (pt < s)));
-        d += __popc((uint32_t)(__builtin_amdgcn_ballot_w64(c) >> (16 * gw)) & 0xFFFFu);
+      if (s - f - 1 > kLongSpan || f + 1 < rlo) {
+        longs[atomicAdd(&nlong, 1)] = it;
+        continue;
       }
-      if (j == 0) items[it].y = (((uint32_t)item.y & 3) == kRem) ? -d : d;
+      const int32_t ns1 = -s - 1;
+      int32_t d = 0;
+      for (int32_t z = f + 1; z < s; z++) {
+        const int32_t q = ring[z & (RING - 1)];
+        d += ((uint32_t)q < (uint32_t)s || q < ns1) ? 1 : 0;
+      }
+      items[it].y = (((uint32_t)item.y & 3) == kRem) ? -d : d;
+    }
+    __syncthreads();
+    // long spans, and spans that reach behind the ring (entries older than ~1 K come from
+    // memory): one wave per item
+    for (int32_t li = wave_id(); li < nlong; li += 4) {
+      const int32_t it = longs[li];
+      const int2 item = items[it];
+      const int32_t s = item.x, f = (int32_t)((uint32_t)item.y >> 2);
+      const int32_t ns1 = -s - 1;
+      int32_t d = 0;
+      for (int32_t z0 = f + 1; z0 < s; z0 += 64) {
+        const int32_t z = z0 + lane_id();
+        bool c = false;
+        if (z < s) {
+          const int32_t q = z >= rlo ? ring[z & (RING - 1)] : delta_word(sq[z]);
+          c = (uint32_t)q < (uint32_t)s || q < ns1;
+        }
+        d += __popcll(__builtin_amdgcn_ballot_w64(c));
+      }
+      if (lane_id() == 0) items[it].y = (((uint32_t)item.y & 3) == kRem) ? -d : d;
     }
     __syncthreads();
     for (int32_t q = threadIdx.x; q < tot; q += 256) {  // the round's pairs, coalesced
