@@ -495,8 +495,12 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int32_t* d_inv = c->buf<int32_t>("inv", N);
   uint64_t* d_skey = c->buf<uint64_t>("skey", N);
   if (c->rank_tier == 0)
+  {
     c->launch(K_WINDOW_RANK, k_window_rank, dim3((unsigned)NSmax), dim3(256), s, d_units, (const SortTile*)d_st,
               (const uint64_t*)d_mkey, d_cord, d_inv, d_skey);
+    c->launch(K_WINDOW_RANK, k_window_rank_wide, dim3((unsigned)lbn), dim3(256), s, d_units, (const uint64_t*)d_mkey, d_cord,
+              d_inv, d_skey);
+  }
   uint64_t* d_ep_rank = c->buf<uint64_t>("ep_rank", N);
   uint64_t* d_ep_clk = c->buf<uint64_t>("ep_clk", N);
   int32_t* d_segend = c->buf<int32_t>("segend", N);

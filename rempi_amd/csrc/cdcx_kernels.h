@@ -33,6 +33,7 @@ __global__ void k_units_lb(const Chunk*, int32_t, const int64_t*, const int32_t*
                            const int32_t*, int2*, int32_t*, int64_t*);
 __global__ void k_unit_prep(Unit*, const TRec*, uint64_t*, int32_t*, int32_t*, int32_t*, uint64_t*, uint32_t*);
 __global__ void k_window_rank(Unit*, const SortTile*, const uint64_t*, int32_t*, int32_t*, uint64_t*);
+__global__ void k_window_rank_wide(Unit*, const uint64_t*, int32_t*, int32_t*, uint64_t*);
 __global__ void k_sort_tiles(const Unit*, const SortTile*, const uint64_t*, uint64_t*, int32_t*, uint64_t*);
 __global__ void k_rank_tiles(const Unit*, const SortTile*, const uint64_t*, const uint64_t*, const int32_t*,
                              const uint64_t*, int32_t*, int32_t*, uint64_t*);

@@ -431,25 +431,21 @@ __global__ void __launch_bounds__(256) k_unit_prep(Unit* __restrict__ units, con
 //                      and ~0 for those after it)
 // where "ordered before" is (key, index) order.  One pass, no sort: each tile of 1024 events
 // loads its events plus a halo of 2D + 1 before and D after, checks the condition for its
-// events (a key equal to the ~0 sentinel fails it too) and writes cord / inv / skey.  A unit
-// with any failing tile is flagged (Unit::wfail); the host ranks it again with the tile sort
-// below, launched over the flagged units' tiles only.
-__global__ void __launch_bounds__(256) k_window_rank(Unit* __restrict__ units, const SortTile* __restrict__ st,
-                                                     const uint64_t* __restrict__ mkey, int32_t* __restrict__ cord,
-                                                     int32_t* __restrict__ inv, uint64_t* __restrict__ skey) {
-  constexpr int D = kRankWin;
+// events (a key equal to the ~0 sentinel fails it too) and writes cord / inv / skey.  The cost
+// is linear in D, so every unit first tries D = 48 and only a unit with a failing tile repeats
+// with D = kRankWin.  A unit that fails that too is flagged (Unit::wfail = 1); the host ranks
+// it again with the tile sort below, launched over the flagged units' tiles only.
+namespace {
+// One attempt with window D.  Returns (to every thread) whether the condition failed for any
+// event of the tile; the ranks of the tile are left in rk[] and own[] holds the thread's keys.
+template <int D>
+__device__ __forceinline__ bool window_rank_try(const Unit& u, int32_t t0, int len, const uint64_t* __restrict__ mkey,
+                                                uint64_t* xk, int32_t* rk, uint64_t (&own)[4]) {
   constexpr int H = 2 * D + 1;  // halo before the tile
   constexpr int NX = H + kSortTile + D;
   static_assert(D % 4 == 0 && D >= 8, "bulk loops run D - 4 iterations, unrolled by 4");
   // Key k of the tile's range sits at xk[k + k / 4]: a thread reads keys 4t + x, and the pad
   // turns its 32 B lane stride into 40 B (10 banks), so 32 lanes read distinct banks.
-  __shared__ uint64_t xk[NX + NX / 4 + 1];
-  __shared__ int32_t rk[kSortTile];
-  const SortTile w = st[blockIdx.x];
-  if (w.unit < 0) return;  // past the batch's sort tiles (the grid is an upper bound)
-  const Unit u = units[w.unit];
-  const int32_t t0 = w.tile * kSortTile;
-  const int len = min(kSortTile, u.M - t0);
   for (int k = threadIdx.x; k < NX; k += 256) {
     const int32_t q = t0 - H + k;
     xk[k + (k >> 2)] = q < 0 ? 0ull : (q >= u.M ? ~0ull : mkey[u.a + q]);
@@ -458,7 +454,6 @@ __global__ void __launch_bounds__(256) k_window_rank(Unit* __restrict__ units, c
   const int L = 4 * threadIdx.x;  // own events: tile offsets L..L+3 = keys L + H + j
   const uint64_t* x0 = xk + 5 * threadIdx.x;
   auto key = [&](int x) { return x0[x + (x >> 2)]; };  // key L + x (x >= 0)
-  uint64_t own[4];
 #pragma unroll
   for (int j = 0; j < 4; j++) own[j] = key(H + j);
   // check: event j's window is keys L + j .. L + j + D (positions p - 2D - 1 .. p - D - 1);
@@ -514,16 +509,69 @@ __global__ void __launch_bounds__(256) k_window_rank(Unit* __restrict__ units, c
     for (int j = e; j < 4; j++) cnt[j] += v < own[j] ? 1 : 0;
   }
 #pragma unroll
+  for (int j = 0; j < 4; j++) rk[L + j] = t0 + L + j - D + cnt[j];
+  return __syncthreads_or(bad);
+}
+}  // namespace
+
+namespace {
+// Ranks one tile with window D and writes cord / inv / skey; returns whether the condition
+// failed for any of its events (then what it wrote is not to be used).
+template <int D>
+__device__ __forceinline__ bool window_rank_tile(const Unit& u, int32_t tile, const uint64_t* __restrict__ mkey,
+                                                 int32_t* __restrict__ cord, int32_t* __restrict__ inv,
+                                                 uint64_t* __restrict__ skey, uint64_t* xk, int32_t* rk) {
+  const int32_t t0 = tile * kSortTile;
+  const int len = min(kSortTile, u.M - t0);
+  uint64_t own[4];
+  const bool bad = window_rank_try<D>(u, t0, len, mkey, xk, rk, own);
+  const int L = 4 * threadIdx.x;
+#pragma unroll
   for (int j = 0; j < 4; j++) {
-    const int32_t r = t0 + L + j - D + cnt[j];
-    rk[L + j] = r;
     if (L + j < len) {
+      const int32_t r = rk[L + j];
       inv[u.a + r] = t0 + L + j;
       skey[u.a + r] = own[j];
     }
   }
-  if (__syncthreads_or(bad) && threadIdx.x == 0) units[w.unit].wfail = 1;
   for (int k = threadIdx.x; k < len; k += 256) cord[u.a + t0 + k] = rk[k];
+  return bad;
+}
+constexpr int kRankNarrow = 48;
+}  // namespace
+
+// First attempt, one block per tile, narrow window.  A remote violation can change the rank
+// of an event whose own neighbourhood is in order, so a failing tile sends its whole unit to
+// the wide window (Unit::wfail bit 2).
+__global__ void __launch_bounds__(256) k_window_rank(Unit* __restrict__ units, const SortTile* __restrict__ st,
+                                                     const uint64_t* __restrict__ mkey, int32_t* __restrict__ cord,
+                                                     int32_t* __restrict__ inv, uint64_t* __restrict__ skey) {
+  constexpr int NX = 2 * kRankNarrow + 1 + kSortTile + kRankNarrow;
+  __shared__ uint64_t xk[NX + NX / 4 + 1];
+  __shared__ int32_t rk[kSortTile];
+  const SortTile w = st[blockIdx.x];
+  if (w.unit < 0) return;  // past the batch's sort tiles (the grid is an upper bound)
+  const Unit u = units[w.unit];
+  if (window_rank_tile<kRankNarrow>(u, w.tile, mkey, cord, inv, skey, xk, rk) && threadIdx.x == 0)
+    atomicOr(&units[w.unit].wfail, 4);
+}
+
+// Second attempt, one block per unit that the narrow window could not rank: all its tiles
+// again with D = kRankWin.  A unit that fails here too keeps wfail bit 0 for the tile sort.
+__global__ void __launch_bounds__(256) k_window_rank_wide(Unit* __restrict__ units, const uint64_t* __restrict__ mkey,
+                                                          int32_t* __restrict__ cord, int32_t* __restrict__ inv,
+                                                          uint64_t* __restrict__ skey) {
+  constexpr int NX = 2 * kRankWin + 1 + kSortTile + kRankWin;
+  __shared__ uint64_t xk[NX + NX / 4 + 1];
+  __shared__ int32_t rk[kSortTile];
+  const Unit u = units[blockIdx.x];
+  if (!(u.wfail & 4)) return;
+  bool bad = false;
+  for (int32_t tile = 0; tile * kSortTile < u.M; tile++) {
+    bad |= window_rank_tile<kRankWin>(u, tile, mkey, cord, inv, skey, xk, rk);
+    __syncthreads();  // rk and xk are reused by the next tile
+  }
+  if (threadIdx.x == 0) units[blockIdx.x].wfail = bad ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------------------
