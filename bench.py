@@ -240,11 +240,16 @@ class Lane:
         self.cdcx.stream_destroy(self.stream)
 
 
+STAGGER_S = float(os.environ.get("CDCX_BENCH_STAGGER_MS", "0")) / 1e3  # experiment: lane k starts k * this later
+
+
 def run_lanes(lanes, fn, steps):
     errs = []
 
     def body(ln):
         try:
+            if STAGGER_S:
+                time.sleep(STAGGER_S * lanes.index(ln))
             for _ in range(steps):
                 fn(ln)
             ln.cdcx.stream_sync(ln.stream)

@@ -182,6 +182,8 @@ struct cdcx_ctx {
   // blocks of the 16-lane chain tier (a work queue: fewer blocks leave CUs to other streams)
   int64_t chain_grid = getenv("CDCX_CHAIN_GRID") ? std::max(1, atoi(getenv("CDCX_CHAIN_GRID"))) : 2048;
   bool chain_g16 = getenv("CDCX_CHAIN_G16") != nullptr;  // first tier on 16-lane groups (A/B timing)
+  // segments of at least this many events run at raised wave priority in the 8-lane chain tier
+  int chain_long = getenv("CDCX_CHAIN_LONG") ? atoi(getenv("CDCX_CHAIN_LONG")) : 1536;
   int64_t chain_tier_counts[3] = {0, 0, 0};  // segments entering each tier in the last encode
 
   template <class T>
@@ -420,7 +422,8 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
             (const int32_t*)d_ntiles, (const int32_t*)d_nsets, (const int32_t*)d_setlist, d_base, d_tstart, d_prevm);
   // (the scatter also forms the records' length increments and their tile sums)
   c->launch(K_SCATTER, k_scatter, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, (const int16_t*)d_dense,
-            (const int32_t*)d_base, (const uint8_t*)d_prevm, (const int64_t*)d_rec_off, d_trec, d_t2s, d_inc0, d_tsum);
+            (const int32_t*)d_base, (const uint8_t*)d_prevm, (const int32_t*)d_nsets, (const int64_t*)d_rec_off, d_trec, d_t2s,
+            d_inc0, d_tsum);
   c->launch(K_RANK_SCAN, k_rank_scan, dim3(R), dim3(256), s, (const int32_t*)d_tsum, (const int32_t*)d_tile0,
             (const int32_t*)d_ntiles, d_toff, d_rtot);
   c->launch(K_CHUNKS, k_chunks, dim3(R), dim3(64), s, d_rec, (const int64_t*)d_rec_off, (const int64_t*)d_nrec,
@@ -617,7 +620,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
         c->launch(K_CHAIN_G8, k_chain_grp8,
                   dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(c->chain_grid, blocks(n, 128)))), dim3(256), s,
                   (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,
-                  d_topg, d_qn, d_ovf1, d_cnt + 1, d_err);
+                  d_topg, d_qn, d_ovf1, d_cnt + 1, (int32_t)c->chain_long, d_err);
       list = d_ovf1;
       nlist = d_cnt + 1;
     }

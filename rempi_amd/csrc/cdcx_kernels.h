@@ -23,8 +23,8 @@ __global__ void k_set_dense(const uint32_t*, int16_t*, int32_t*, int32_t*);
 __global__ void k_tile_hist(const int32_t*, const Tile*, uint32_t*, uint32_t*, uint32_t*);
 __global__ void k_hist_scan(const uint32_t*, const int32_t*, const int32_t*, const int32_t*, const int32_t*, int32_t*,
                             int32_t*, uint8_t*);
-__global__ void k_scatter(const int32_t*, const Tile*, const int16_t*, const int32_t*, const uint8_t*, const int64_t*,
-                          TRec*, int32_t*, uint8_t*, int32_t*);
+__global__ void k_scatter(const int32_t*, const Tile*, const int16_t*, const int32_t*, const uint8_t*, const int32_t*,
+                          const int64_t*, TRec*, int32_t*, uint8_t*, int32_t*);
 __global__ void k_rank_scan(const int32_t*, const int32_t*, const int32_t*, int32_t*, int32_t*);
 __global__ void k_chunks(const int32_t*, const int64_t*, const int64_t*, const int32_t*, const int32_t*, const int32_t*,
                          const uint8_t*, const int32_t*, const int32_t*, const int32_t*, const int64_t*, int64_t, int2*,
@@ -53,7 +53,7 @@ __global__ void k_chain_grp(const Unit*, Seg*, const int32_t*, const int32_t*, c
                             int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*);
 // chain_group8.hip
 __global__ void k_chain_grp8(const Unit*, Seg*, const int32_t*, const int32_t*, const int32_t*, const int32_t*, int32_t*,
-                             int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, uint32_t*);
+                             int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t, uint32_t*);
 __global__ void k_chain_exits(const Unit*, const Seg*, int32_t, const int32_t*, const int32_t*, const int32_t*, int32_t*,
                               uint32_t*);
 __global__ void k_chain_entries(Unit*, int32_t, Seg*, const int32_t*);

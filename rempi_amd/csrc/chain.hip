@@ -490,11 +490,12 @@ __global__ void __launch_bounds__(256) k_chain_mark(const Unit* __restrict__ uni
                                                     const int32_t* __restrict__ qn, uint8_t* __restrict__ chain) {
   const int32_t nw = gridDim.x * 4;
   const int l = lane_id();
-  for (int32_t si = blockIdx.x * 4 + wave_id(); si < nsegs; si += nw) {
+  for (int32_t si = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wave_id()); si < nsegs; si += nw) {
     const Seg sg = segs[si];
     const int64_t a = units[sg.unit].a;
     const int32_t s0 = sg.start, s1 = sg.start + sg.len;
-    int32_t want = qn[a + s0 + sg.entry];
+    // (kept in a scalar register: the walk below is wave-uniform, one v_readlane per chain node)
+    int32_t want = __builtin_amdgcn_readfirstlane(qn[a + s0 + sg.entry]);
     for (int32_t c0 = s0 + ((s1 - 1 - s0) & ~63); c0 >= s0; c0 -= 64) {
       const int32_t r = c0 + l;
       const int32_t pv = (r < s1) ? par[a + r] : 0;

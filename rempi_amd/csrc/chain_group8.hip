@@ -37,7 +37,6 @@ namespace cdcx {
 namespace {
 constexpr int G8 = 8;
 constexpr int kRing8 = 64;      // rows of {par, column} per group in LDS
-constexpr int kLongSeg = 1536;  // events: segments from here on run at raised wave priority
 
 using mask64 = unsigned long long;
 // lane masks of a signed compare, straight from v_cmp (LLVM integer predicates)
@@ -93,7 +92,8 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
                                                     const int32_t* __restrict__ cord, const int32_t* __restrict__ opn,
                                                     int32_t* __restrict__ par, int32_t* __restrict__ exta,
                                                     int32_t* __restrict__ topg, int32_t* __restrict__ qn,
-                                                    int32_t* __restrict__ ovf, int32_t* __restrict__ novf, uint32_t* err) {
+                                                    int32_t* __restrict__ ovf, int32_t* __restrict__ novf, int32_t long_len,
+                                                    uint32_t* err) {
   constexpr int G = G8;
   constexpr int kGroups = 256 / G;
   constexpr int R = kRing8;
@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
       i = s0;
       rj = s0 - t + j;
       nl = lmax = nrel1 = qcnt = 0;
-      islong = sg.len >= kLongSeg;
+      islong = sg.len >= long_len;
       cw0 = (j < G - t && s0 + j < s1) ? ldg(opn, tb + 4u * j) : 0;
       cw1 = (rj + G < s1) ? ldg(opn, ab + 4u * (uint32_t)(rj + G)) : 0;
     }

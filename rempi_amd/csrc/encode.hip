@@ -98,8 +98,8 @@ __global__ void __launch_bounds__(256) k_hist_scan(const uint32_t* __restrict__ 
 }
 
 // Stable scatter of records into T-order.  Rounds of 256 consecutive records; within a
-// wave, records with the same table find each other with 8 ballots (one per bit of the
-// table index), which keeps the partition stable for any number of tables.
+// wave, records with the same table find each other with one ballot per bit of the rank's
+// table indexes, which keeps the partition stable for any number of tables.
 //
 // The same pass forms inc0, the length increment of each record if chunks were infinite
 // (add(), :189-212): 1 for a matched event, 1 for an unmatched event that starts a new run of
@@ -110,9 +110,10 @@ __global__ void __launch_bounds__(256) k_hist_scan(const uint32_t* __restrict__ 
 // contiguous from a kTile-aligned start; tsum = the tile's sum.
 __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
                                                  const int16_t* __restrict__ dense, const int32_t* __restrict__ base,
-                                                 const uint8_t* __restrict__ prevm, const int64_t* __restrict__ rec_off,
-                                                 TRec* __restrict__ trec, int32_t* __restrict__ t2s,
-                                                 uint8_t* __restrict__ inc0s, int32_t* __restrict__ tsum) {
+                                                 const uint8_t* __restrict__ prevm, const int32_t* __restrict__ nsets,
+                                                 const int64_t* __restrict__ rec_off, TRec* __restrict__ trec,
+                                                 int32_t* __restrict__ t2s, uint8_t* __restrict__ inc0s,
+                                                 int32_t* __restrict__ tsum) {
   constexpr int ROUNDS = kTile / 256;
   __shared__ int32_t wc[ROUNDS * 4 * kMaxSets];  // [round][wave][table]: count | last record's flags << 16
   __shared__ int32_t lds[4];
@@ -120,6 +121,8 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
   const Tile t = tiles[blockIdx.x];
   const int w = wave_id(), l = lane_id();
   const uint64_t lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
+  const int T = nsets[t.rank];
+  const int tbits = T > 1 ? 32 - __clz(T - 1) : 0;  // bits of a table index of this rank
   int4 lo[ROUNDS], hi[ROUNDS];
 #pragma unroll
   for (int j = 0; j < ROUNDS; j++) {
@@ -144,8 +147,7 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
     const int32_t sid = hi[j].w;
     const int tb = valid ? dense[t.rank * kMaxSets + ((uint32_t)sid < (uint32_t)kMaxSets ? sid : 0)] : 0;
     uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
-#pragma unroll
-    for (int b = 0; b < 8; b++) {
+    for (int b = 0; b < tbits; b++) {
       uint64_t m = __builtin_amdgcn_ballot_w64(((tb >> b) & 1) != 0);
       peers &= ((tb >> b) & 1) ? m : ~m;
     }

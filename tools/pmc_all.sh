@@ -1,6 +1,7 @@
 #!/bin/bash
 # One rocprofv3 --pmc pass per counter group over EVERY kernel of a small bench run (run on the
-# GPU box): tools/pmc_all.sh <outdir> [bench args...]; summary by tools/pmc_table.py.
+# GPU box): tools/pmc_all.sh <outdir> [bench args...]; summary by tools/pmc_table.py (per record
+# of the default 8 ranks x 10 M events; PMC_RECORDS overrides the count).
 set -o pipefail
 OUT=${1:-gpurun_out/pmc_all}; shift 1
 mkdir -p $OUT
@@ -11,4 +12,4 @@ for set in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_V
   i=$((i+1))
   timeout -s KILL 150 rocprofv3 --pmc $set -d $OUT/p$i -o run --output-format csv -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
-python3 tools/pmc_table.py $OUT
+python3 tools/pmc_table.py $OUT ${PMC_RECORDS:-80000000} $OUT/pmc_traffic.json
