@@ -70,7 +70,7 @@ inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 // encode and decode never overlap): grow-only named buffers shared by both phases.
 constexpr const char* kAliasRecs = "trec";    // decoded records       <- T-order records
 constexpr const char* kAliasIdd = "mkey";     // pair ids              <- observed-order keys
-constexpr const char* kAliasDld = "skey";     // pair delays           <- clock-order keys
+constexpr const char* kAliasDld = "seq";      // pair delays           <- edit sequence (the clock-order keys, "skey", are the decoder's input)
 constexpr const char* kAliasWpd = "run_cnt";  // with_previous         <- unmatched run counts
 constexpr const char* kAliasUidd = "ep_rank"; // unmatched ids         <- epoch ranks
 constexpr const char* kAliasPerm = "cord";    // perm                  <- clock order of rows
@@ -180,7 +180,7 @@ struct cdcx_ctx {
   // 1: every unit takes the tile sort (skips the windowed rank), for tests
   int rank_tier = getenv("CDCX_RANK_TIER") ? atoi(getenv("CDCX_RANK_TIER")) : 0;
   // blocks of the 16-lane chain tier (a work queue: fewer blocks leave CUs to other streams)
-  int64_t chain_grid = getenv("CDCX_CHAIN_GRID") ? std::max(1, atoi(getenv("CDCX_CHAIN_GRID"))) : 2048;
+  int64_t chain_grid = getenv("CDCX_CHAIN_GRID") ? std::max(1, atoi(getenv("CDCX_CHAIN_GRID"))) : 1280;
   bool chain_g16 = getenv("CDCX_CHAIN_G16") != nullptr;  // first tier on 16-lane groups (A/B timing)
   // segments of at least this many events run at raised wave priority in the 8-lane chain tier
   int chain_long = getenv("CDCX_CHAIN_LONG") ? atoi(getenv("CDCX_CHAIN_LONG")) : 1536;
@@ -662,7 +662,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   uint32_t* d_seq = c->buf<uint32_t>("seq", 2 * N);
   int32_t* d_sx = c->buf<int32_t>("sx", 2 * N);
   c->launch(K_POSITIONS, k_pos_rows, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_cord,
-            (const uint8_t*)d_chain, d_posA, d_crow, d_seq);
+            (const uint8_t*)d_chain, d_posA, d_crow);
   c->launch(K_POSITIONS, k_pos_cols, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_inv,
             (const uint8_t*)d_chain, (const int32_t*)d_posA, (const int32_t*)d_crow, d_seq, d_sx);
   d_pid = c->buf<int32_t>("pid", N);
@@ -676,7 +676,8 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   const int64_t total_max = 8ll * C + 72ll * NU + 16ll * tot.sources + foot_max +
                             (c->rep ? 0 : 8ll * tot.with_next + 16ll * tot.matched + 16ll * tot.runs);
   uint8_t* d_out = c->buf<uint8_t>("out", total_max);
-  int2* d_keys = c->buf<int2>("keys", key_run);
+  // the units' clock-ordered keys, dense in file order since the rank pass: the replay side's key stream
+  int2* d_keys = reinterpret_cast<int2*>(d_skey);
   int64_t* d_upre = c->buf<int64_t>("upre", (size_t)NU + 1);
   int64_t* d_cpre = c->buf<int64_t>("cpre", (size_t)C + 1);
   int64_t* d_files = c->buf<int64_t>("file_layout", 3 * (size_t)R + 1);  // file_off[R], file_len[R], foot_off[R], total
@@ -690,7 +691,6 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   c->launch(K_FOOTER_WRITE, k_footer_write, dim3(blocks(R, 64)), dim3(64), s, (const int64_t*)d_fk_off,
             (const int64_t*)d_fb_off, (const uint64_t*)d_fkey, (const int32_t*)d_fnext, (const int32_t*)d_fbucket,
             (const int32_t*)d_fcount, (const int64_t*)(d_files + 2 * R), R, d_out);
-  c->launch(K_WRITE_KEYS, k_write_keys, dim3(NU), dim3(256), s, (const Unit*)d_units, (const uint64_t*)d_skey, d_keys);
   {  // wait 4: error word, file offsets and lengths
     Mail m(c, s, 64 + 8 * (3 * (size_t)R + 1));
     const size_t o_err = m.add(d_err, 4), o_f = m.add(d_files, 8 * (3 * (size_t)R + 1));

@@ -88,6 +88,11 @@ __device__ __host__ __forceinline__ uint64_t pack_key(int32_t clk, int32_t src) 
 __device__ __host__ __forceinline__ int32_t key_clock(uint64_t k) { return (int32_t)((uint32_t)(k >> 32) ^ 0x80000000u); }
 __device__ __host__ __forceinline__ int32_t key_source(uint64_t k) { return (int32_t)((uint32_t)k ^ 0x80000000u); }
 
+// The same key as the two signed words {source, clock} (an int2 in memory): the form in which
+// a unit's keys are kept in clock order, at Unit::key_off, and handed to the replay side.
+constexpr uint64_t kKeyBias = 0x8000000080000000ull;
+__device__ __host__ __forceinline__ uint64_t key_words(uint64_t k) { return k ^ kKeyBias; }
+
 __device__ __forceinline__ uint64_t sext(int32_t v) { return (uint64_t)(int64_t)v; }
 
 // Unaligned-safe 8-byte little-endian store into the byte output (all CDC sections are

@@ -58,7 +58,7 @@ __global__ void k_chain_exits(const Unit*, const Seg*, int32_t, const int32_t*, 
                               uint32_t*);
 __global__ void k_chain_entries(Unit*, int32_t, Seg*, const int32_t*);
 __global__ void k_chain_mark(const Unit*, const Seg*, int32_t, const int32_t*, const int32_t*, uint8_t*);
-__global__ void k_pos_rows(const Unit*, const int32_t*, const uint8_t*, int32_t*, int32_t*, uint32_t*);
+__global__ void k_pos_rows(const Unit*, const int32_t*, const uint8_t*, int32_t*, int32_t*);
 __global__ void k_pos_cols(const Unit*, const int32_t*, const uint8_t*, const int32_t*, const int32_t*, uint32_t*,
                            int32_t*);
 __global__ void k_deltas(const Unit*, const uint32_t*, const int32_t*, int32_t*, int32_t*);
@@ -69,7 +69,6 @@ __global__ void k_footer_order(const Unit*, const int32_t*, const int32_t*, cons
                                const int64_t*, uint64_t*, int32_t*, int32_t*, int32_t*);
 __global__ void k_footer_write(const int64_t*, const int64_t*, const uint64_t*, const int32_t*, const int32_t*,
                                const int32_t*, const int64_t*, int32_t, uint8_t*);
-__global__ void k_write_keys(const Unit*, const uint64_t*, int2*);
 
 // lists.hip
 __global__ void k_build_tiles(const int64_t*, const int32_t*, Tile*);

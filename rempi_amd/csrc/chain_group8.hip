@@ -21,7 +21,13 @@
 //    launches this kernel only when the batch has fewer than 2^30 rows;
 //  * group ballots as scalar compare masks (no select/compare round trip per ballot);
 //  * ancestor climbs read the LDS ring directly; the global fallback for rows older than the
-//    ring sits behind a branch.
+//    ring sits behind a branch;
+//  * the single-word outputs are combined in LDS: the spilled tops (levels below the eight in
+//    registers) live in a per-group ring of the last 32 spilled levels that is written to
+//    topg one whole 128-byte line at a time, and never at all for levels that are still in
+//    the ring when the segment ends; the max-level rows (qn) are kept in LDS and stored once
+//    at the end of the segment.  One word at a time, these stores left partly written lines
+//    in more groups than the L2 holds and went to memory several times per line.
 //
 // 8-lane groups on 16-lane DPP rows: a row shift leaks one value of the neighbouring group
 // into lane 7 (row_shl) or lane 0 (row_shr) of a group; every use below either overwrites
@@ -37,6 +43,8 @@ namespace cdcx {
 namespace {
 constexpr int G8 = 8;
 constexpr int kRing8 = 64;      // rows of {par, column} per group in LDS
+constexpr int kTopRing = 32;    // spilled tops per group in LDS: one 128-byte line of topg
+constexpr int kQBuf = 8;        // max-level rows per group kept in LDS until the segment ends
 
 using mask64 = unsigned long long;
 // lane masks of a signed compare, straight from v_cmp (LLVM integer predicates)
@@ -100,8 +108,12 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
   __shared__ int32_t next_j;
   __shared__ int2 ring_all[kGroups][R];          // {par, column} of row r at [r % R]
   __shared__ int32_t comp_all[kGroups][3 * 16];  // sweep compaction of a list that uses the B slots
+  __shared__ int32_t tring_all[kGroups][kTopRing];  // spilled top of level e + 1 at [(tq + e) % 32]
+  __shared__ int32_t qbuf_all[kGroups][kQBuf];
   int2* ring = ring_all[threadIdx.x / G];
   int32_t* comp = comp_all[threadIdx.x / G];
+  int32_t* tring = tring_all[threadIdx.x / G];
+  int32_t* qbuf = qbuf_all[threadIdx.x / G];
   if (threadIdx.x == 0) next_j = 0;
   __syncthreads();
 
@@ -112,6 +124,7 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
   // group-uniform state.  ab / tb: byte offsets of the unit's row 0 / the segment's row 0.
   int32_t si = -1, s0 = 0, s1 = 0, ord = 0;
   uint32_t ab = 0, tb = 0;
+  int32_t tq = 0;  // word index of the segment's topg row 0 (tb / 4): lines of topg are 32-word aligned in it
   int32_t i = 0, nl = 0, lmax = 0, nrel1 = 0, qcnt = 0;
   bool islong = false;
   // lane state: leaf slots j (A) and 8 + j (B), top of level lmax - j, the row window (row
@@ -157,6 +170,7 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
       G8_STAT(1);
       if (si >= 0) {
         if (j < t && rj >= s0) stg(par, ab + 4u * (uint32_t)rj, pval);
+        if (j < min(qcnt, kQBuf)) stg(qn, tb + 4u * (uint32_t)j, qbuf[j]);
         if (j == 0) {
           segs[si].lmax = lmax;
           segs[si].qcount = qcnt;
@@ -175,6 +189,7 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
       s1 = sg.start + sg.len;
       ord = sg.ord;
       tb = ab + 4u * (uint32_t)s0;
+      tq = (int32_t)(tb >> 2);
       i = s0;
       rj = s0 - t + j;
       nl = lmax = nrel1 = qcnt = 0;
@@ -202,7 +217,11 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
       while (lo <= hi) {
         G8_STAT(5);
         const int32_t mid = (lo + hi) >> 1;
-        if (ldg(topg, tb + 4u * (uint32_t)mid - 4u) < c) {
+        // level mid = spill index mid - 1; the last kTopRing spilled levels are in the ring
+        int32_t tv = tring[(tq + mid - 1) & (kTopRing - 1)];
+        asm volatile("" : "+v"(tv));
+        if (mid - 1 < lmax - G - kTopRing) tv = ldg(topg, tb + 4u * (uint32_t)mid - 4u);
+        if (tv < c) {
           ks = mid;
           lo = mid + 1;
         } else {
@@ -299,14 +318,39 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
     const bool grow = k > lmax;
     if (grow && lmax >= G) G8_STAT(12);
     if (!grow && lmax - k >= G) G8_STAT(13);
-    if (grow && j == G - 1 && lmax >= G) stg(topg, tb + 4u * (uint32_t)lmax - 4u * G, top);
-    if (!grow && lmax - k >= G && j == 0) stg(topg, tb + 4u * (uint32_t)k - 4u, c);
+    if (grow && lmax >= G) {
+      // spill index e = lmax - G (level e + 1) leaves the registers: into the ring, and the
+      // line of topg that it completes goes to memory whole (words before the segment's
+      // first belong to another segment's spill area and are left alone)
+      const int32_t e = lmax - G;
+      const int32_t w = (tq + e) & (kTopRing - 1);
+      if (j == G - 1) tring[w] = top;
+      if (w == kTopRing - 1) {
+#pragma unroll
+        for (int q = 0; q < kTopRing / G; q++) {
+          const int32_t z = q * G + j;  // word of the line
+          const int32_t ez = e - (kTopRing - 1) + z;
+          const int32_t v = tring[z];
+          if (ez >= 0) stg(topg, tb + 4u * (uint32_t)ez, v);
+        }
+      }
+    }
+    if (!grow && lmax - k >= G && j == 0) {
+      // a spilled level gets a new top: in the ring while it is among the last kTopRing
+      // spilled, and in memory when its line has been written already
+      const int32_t e = k - 1, n = lmax - G;  // n spilled levels so far
+      if (e >= n - kTopRing) tring[(tq + e) & (kTopRing - 1)] = c;
+      if (e < ((tq + n) & ~(kTopRing - 1)) - tq) stg(topg, tb + 4u * (uint32_t)e, c);
+    }
     const int32_t tshift = prev8(top);
     top = grow ? ((j == 0) ? c : tshift) : ((j == lmax - k) ? c : top);
     qcnt = grow ? 0 : qcnt;
     lmax = grow ? k : lmax;
     if (k == lmax) G8_STAT(14);
-    if (k == lmax && j == 0) stg(qn, tb + 4u * (uint32_t)qcnt, i);
+    if (k == lmax && j == 0) {
+      if (qcnt < kQBuf) qbuf[qcnt] = i;
+      else stg(qn, tb + 4u * (uint32_t)qcnt, i);
+    }
     qcnt += (k == lmax) ? 1 : 0;
 
     // ---- leaves: drop the adopted one, sweep, append the new node --------------------------

@@ -533,7 +533,7 @@ __device__ __forceinline__ bool window_rank_tile(const Unit& u, int32_t tile, co
     if (L + j < len) {
       const int32_t r = rk[L + j];
       inv[u.a + r] = t0 + L + j;
-      skey[u.a + r] = own[j];
+      skey[u.key_off + r] = key_words(own[j]);
     }
   }
   for (int k = threadIdx.x; k < len; k += 256) cord[u.a + t0 + k] = rk[k];
@@ -772,7 +772,7 @@ __global__ void __launch_bounds__(256) k_rank_tiles(const Unit* __restrict__ uni
     }
     cord[u.a + i] = rank;
     inv[u.a + rank] = i;
-    skey[u.a + rank] = x;
+    skey[u.key_off + rank] = key_words(x);
   }
 }
 
@@ -798,7 +798,7 @@ __global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const u
   Unit& u = units[blockIdx.x];
   if (u.wfail != 0) return;  // not ranked yet (k_window_rank), or already done
   if (kBig && u.S != -1) return;
-  const int64_t a = u.a;
+  const int64_t a = u.a, ka = u.key_off;
   const int32_t M = u.M;
   for (int i = threadIdx.x; i < HCAP; i += 256) {
     hsrc[i] = INT32_MIN;
@@ -808,9 +808,9 @@ __global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const u
   if (threadIdx.x == 0) nlist = 0;
   __syncthreads();
   for (int32_t r = threadIdx.x; r < M; r += 256) {
-    const uint64_t k = skey[a + r];
+    const uint64_t k = key_words(skey[ka + r]);  // (skey holds {source, clock} words)
     const int32_t src = key_source(k), clk = key_clock(k);
-    if (!kBig && r + 1 < M && skey[a + r + 1] == k && clk != 0) raise_error(err, kErrClockOrder);
+    if (!kBig && r + 1 < M && key_words(skey[ka + r + 1]) == k && clk != 0) raise_error(err, kErrClockOrder);
     if (src == INT32_MIN) { raise_error(err, kErrLimit); continue; }
     uint32_t h = ((uint32_t)src * 2654435761u) % HCAP;
     for (int probe = 0; probe < HCAP; probe++) {
@@ -938,18 +938,17 @@ __device__ __forceinline__ int2 block_scan_cnt_max(int2 v, int2* lds, int2* tota
 }  // namespace
 
 // Rows pass (4 rows per thread per round): Kr = #chain rows before r, colprev = last chain
-// column before r.  posA of the IGNORE of chain row r / the ADD of off-chain row r (see
-// above), crow[k] = row of the k-th chain node, and the IGNORE entries of the sequence.
+// column before r.  posA of the ADD of off-chain row r (see above) and crow[k] = row of the
+// k-th chain node.
 __global__ void __launch_bounds__(256) k_pos_rows(const Unit* __restrict__ units, const int32_t* __restrict__ cord,
                                                   const uint8_t* __restrict__ chain, int32_t* __restrict__ posA,
-                                                  int32_t* __restrict__ crow, uint32_t* __restrict__ seq) {
+                                                  int32_t* __restrict__ crow) {
   __shared__ int2 lds[4];
   const Unit u = units[blockIdx.x];
   const int64_t a = u.a;
   const int32_t M = u.M;
   const int32_t* c = cord + a;
   const uint8_t* ch = chain + a;
-  uint32_t* sq = seq + 2 * a;
   int32_t ck = 0, cc = -1;
   for (int32_t b = 0; b < M; b += 1024) {
     const int32_t r0 = b + 4 * threadIdx.x;
@@ -974,10 +973,7 @@ __global__ void __launch_bounds__(256) k_pos_rows(const Unit* __restrict__ units
       const int32_t r = r0 + q;
       if (r < M) {
         if (isc[q]) {
-          const int32_t pa = r + cv[q] - kx;
-          posA[a + r] = pa;
           crow[a + kx] = r;
-          sq[pa] = kIgn;
           kx++;
           cx = cv[q];
         } else {
@@ -991,13 +987,30 @@ __global__ void __launch_bounds__(256) k_pos_rows(const Unit* __restrict__ units
 }
 
 // Columns pass: Kc = #chain columns before j; the REMOVE of off-chain column j sits at
-// rnext(j) + j - Kc with rnext = row of the Kc-th chain node (M past the last).  Writes both
-// entries of every off-chain element x = j: seq = partner position << 2 | type, sx = x.
+// rnext(j) + j - Kc with rnext = row of the Kc-th chain node (M past the last).  Forms both
+// entries of every off-chain element x = j (seq = partner position << 2 | type, sx = x) and
+// the IGNORE of a chain column j (row r = inv[j], Kr(r) = Kc(j)) at r + j - Kc, right after
+// the REMOVEs of its gap: every entry of the sequence comes from this pass.
+//
+// The entries of a round of 1024 columns land within a few dozen positions of one contiguous
+// stretch of the sequence (the REMOVE / IGNORE positions ascend with the column, the ADDs of
+// the same rows fill the gaps between them), but each one is a single word: stored one by
+// one, every store instruction touches a dozen lines and the lines go to memory several times
+// over.  So a round collects its entries in an LDS image of the stretch and writes the image
+// out with consecutive lanes on consecutive words; slots that no entry of this round fills
+// (the ragged ends, which the neighbouring rounds fill) are skipped, and an entry that falls
+// outside the image (a far move) is stored directly -- every position is written exactly once
+// either way.
 __global__ void __launch_bounds__(256) k_pos_cols(const Unit* __restrict__ units, const int32_t* __restrict__ inv,
                                                   const uint8_t* __restrict__ chain, const int32_t* __restrict__ posA,
                                                   const int32_t* __restrict__ crow, uint32_t* __restrict__ seq,
                                                   int32_t* __restrict__ sx) {
+  constexpr int32_t CAP = 2560;   // positions of the image (a round makes ~1.6 K entries)
+  constexpr int32_t SLACK = 256;  // of them, before the round's first REMOVE / IGNORE position
+  constexpr uint32_t kNone = 3u;  // no entry has type 3
   __shared__ int32_t lds[4];
+  __shared__ uint32_t wseq[CAP];
+  __shared__ int32_t wsx[CAP];
   const Unit u = units[blockIdx.x];
   const int64_t a = u.a;
   const int32_t M = u.M, K = u.K;
@@ -1005,6 +1018,18 @@ __global__ void __launch_bounds__(256) k_pos_cols(const Unit* __restrict__ units
   int32_t* sxa = sx + 2 * a;
   int32_t ck = 0;
   for (int32_t b = 0; b < M; b += 1024) {
+    const int32_t base = ((ck < K) ? crow[a + ck] : M) + b - ck - SLACK;  // position of image slot 0
+    for (int32_t z = threadIdx.x; z < CAP; z += 256) wseq[z] = kNone;
+    auto put = [&](int32_t pos, uint32_t e, int32_t x) {
+      const int32_t z = pos - base;
+      if ((uint32_t)z < (uint32_t)CAP) {
+        wseq[z] = e;
+        wsx[z] = x;
+      } else {
+        sq[pos] = e;
+        if ((e & 3u) != kIgn) sxa[pos] = x;
+      }
+    };
     const int32_t j0 = b + 4 * threadIdx.x;
     int32_t row[4];
     bool isc[4];
@@ -1017,22 +1042,30 @@ __global__ void __launch_bounds__(256) k_pos_cols(const Unit* __restrict__ units
       v += (ok && isc[q]) ? 1 : 0;
     }
     int32_t tot;
-    int32_t kc = ck + block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);
+    int32_t kc = ck + block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);  // (barriers: the image is cleared)
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int32_t j = j0 + q;
       if (isc[q]) {
+        if (j < M) put(row[q] + j - kc, kIgn, 0);
         kc++;
         continue;
       }
       const int32_t pr = ((kc < K) ? crow[a + kc] : M) + j - kc;
       const int32_t pa = posA[a + row[q]];
-      sq[pr] = ((uint32_t)pa << 2) | kRem;
-      sxa[pr] = j;
-      sq[pa] = ((uint32_t)pr << 2) | kAdd;
-      sxa[pa] = j;
+      put(pr, ((uint32_t)pa << 2) | kRem, j);
+      put(pa, ((uint32_t)pr << 2) | kAdd, j);
     }
     ck += tot;
+    __syncthreads();
+    for (int32_t z = threadIdx.x; z < CAP; z += 256) {
+      const uint32_t e = wseq[z];
+      if (e != kNone) {
+        sq[base + z] = e;
+        if ((e & 3u) != kIgn) sxa[base + z] = wsx[z];
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -1345,16 +1378,6 @@ __global__ void __launch_bounds__(64) k_footer_write(const int64_t* __restrict__
   const int64_t kb = fk_off[r];
   for (int32_t p = fbucket[fb_off[r]]; p != -1; p = fnext[kb + p], j++) st_u32(o + 16 + 4 * j, (uint32_t)fkey[kb + p]);
   st_u32(o + 16 + 4ull * fcount[r], 0);
-}
-
-// Sorted keys of every unit in file order (the replay side's per-table key stream).
-__global__ void __launch_bounds__(256) k_write_keys(const Unit* __restrict__ units, const uint64_t* __restrict__ skey,
-                                                    int2* __restrict__ keys) {
-  const Unit u = units[blockIdx.x];
-  for (int32_t r = threadIdx.x; r < u.M; r += 256) {
-    const uint64_t k = skey[u.a + r];
-    keys[u.key_off + r] = make_int2(key_source(k), key_clock(k));
-  }
 }
 
 }  // namespace cdcx
