@@ -42,6 +42,8 @@ sys.path.insert(0, ROOT)
 
 RECORD_BYTES = 32
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+SIMDS = 1024           # 256 CUs x 4 SIMDs
+SCLK_HZ = 2.4e9        # engine clock under this load (rocm-smi during the bench: 2.35-2.40 GHz)
 FIXTURE = os.path.join(ROOT, "tests", "golden", "config3_full.json")
 
 
@@ -445,16 +447,34 @@ def main():
     comp_per_event = counters[1] / max(total_records, 1)
 
     # Roofline of the dominant kernel: algorithmic bytes per launch / mean launch duration.
+    # Dominant = the longest launch with the GPU to itself (the solo steps); with all lanes in
+    # flight a launch's duration also counts the time its waves wait for the other lanes'.
     kern = {k: v for k, v in ktimes.items() if v[1] > 0}
-    dom = max(kern, key=lambda k: kern[k][0])
-    dom_ms, dom_launches = kern[dom]
-    if dom in solo:
-        s_ms, s_n = solo[dom]
-        launch_ms, launch_records = s_ms / s_n, solo_records
+    traffic = pmc_traffic() if rank == 0 else None
+
+    def line(k, launch_ms, launch_records):
+        algo = algorithmic_bytes(k, launch_records, comp_per_event)
+        ach = algo / (launch_ms / 1e3) / 1e9
+        d = {"kernel": k, "launch_ms": round(launch_ms, 3), "algorithmic_bytes_per_launch": round(algo),
+             "achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5)}
+        pk = (traffic or {}).get("kernels", {}).get(k)
+        if pk and pk.get("bytes_per_record") is not None:
+            d["traffic"] = round(pk["bytes_per_record"] * launch_records)
+            # vector-instruction issue: wave instructions x 4 cycles on the chip's SIMDs
+            issue_s = pk["valu"] / traffic["records"] * launch_records * 4 / (SIMDS * SCLK_HZ)
+            d["valu_issue_frac"] = round(issue_s / (launch_ms / 1e3), 3)
+        return d
+
+    if solo:
+        per = {k: (v[0] / v[1], solo_records) for k, v in solo.items()}
     else:
-        launch_ms, launch_records = dom_ms / dom_launches, per_launch_records
-    algo = algorithmic_bytes(dom, launch_records, comp_per_event)
-    achieved = algo / (launch_ms / 1e3) / 1e9
+        per = {k: (v[0] / v[1], per_launch_records) for k, v in kern.items()}
+    order = sorted(per, key=lambda k: -per[k][0])
+    dom = order[0]
+    dom_ms, dom_launches = kern.get(dom, (0.0, 0))
+    launch_ms, launch_records = per[dom]
+    dom_line = line(dom, launch_ms, launch_records)
+    top = [line(k, *per[k]) for k in order[:8]]
 
     if args.kernel_report and rank == 0:
         tot = sum(v[0] for v in kern.values())
@@ -475,7 +495,6 @@ def main():
 
     if rank == 0:
         ranks_done = int(counters[6])
-        traffic = pmc_traffic()
         out = {
             "metric": "CDC encode+decode GB/s device-resident, 1024 ranks x 10M events; bit-exact",
             "value": round(value, 3),
@@ -505,19 +524,23 @@ def main():
                                          "permutation for fixture ranks; encode: reference SHA-256 of the rank file "
                                          "for fixture ranks (+ CPU restatement bytes for --oracle-ranks)"},
                        "verify_failures": int(counters[3] + counters[5])},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None if traffic is None or dom not in traffic["kernels"] else
-                         round(traffic["kernels"][dom]["bytes_per_record"] * launch_records),
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": dom_line["achieved"], "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": dom_line["frac"], "traffic": dom_line.get("traffic"),
                          "traffic_source": PMC_TRAFFIC if traffic else None,
                          "launch_ms": round(launch_ms, 3),
-                         "launch_ms_how": "HIP events, one lane alone on the GPU" if dom in solo else
+                         "launch_ms_how": "HIP events, one lane alone on the GPU" if solo else
                                           "HIP events with all lanes in flight",
-                         "launch_ms_concurrent": round(dom_ms / dom_launches, 3),
-                         "algorithmic_bytes_per_launch": round(algo),
+                         "launch_ms_concurrent": round(dom_ms / dom_launches, 3) if dom_launches else None,
+                         "algorithmic_bytes_per_launch": dom_line["algorithmic_bytes_per_launch"],
+                         "valu_issue_frac": dom_line.get("valu_issue_frac"),
+                         "valu_issue_how": f"rocprofv3 SQ_INSTS_VALU per record x records x 4 cycles / ({SIMDS} SIMDs x "
+                                           f"{SCLK_HZ / 1e9} GHz) / launch time: the share of the launch its vector "
+                                           "instructions need at the issue rate of one per 4 cycles per SIMD",
+                         "kernels": top,
                          "pipeline_achieved": round(pipeline_bytes(comp_per_event) * total_records / tmax / 1e9, 2),
                          "pipeline_algorithmic_bytes_per_record": round(pipeline_bytes(comp_per_event), 2),
-                         "pipeline_traffic_per_record": None if traffic is None else traffic.get("pipeline_bytes_per_record")},
+                         "pipeline_traffic_per_record": None if traffic is None else traffic.get("pipeline_bytes_per_record"),
+                         "pipeline_valu_per_record": None if traffic is None else traffic.get("pipeline_valu_per_record")},
             "cpu_baseline": cpu,
             "host_io": host_io,
         }
@@ -548,11 +571,10 @@ def algorithmic_bytes(kernel, n_records, c):
         "k_chain_grp16": m * (4 + 4 + 4),
         "k_chain_grp64": m * (4 + 4 + 4),
         "k_chain_mark": m * (4 + 1),
-        "k_positions": m * (4 + 1 + 4 + 4 + 4) / 2,
+        "k_positions": m * (4 + 1 + 4 + 1.4 + 4 + 1 + 4 + 1.4 + 1.64 * 8) / 2,  # mean of its two launches (rows, columns)
         "k_deltas": m * (1.3 * 4 + 0.64 * (4 + 4 + 4)),
         "k_write_units": m * (4 + 4 + 8) + c,
-        "k_write_keys": m * (8 + 8),
-        "k_dec_sections": 0.3 * c,
+                "k_dec_sections": 0.3 * c,
         "k_dec_perm_grp": m * (0.64 * (8 + 16) + 8),
         "k_dec_records": c + m * (4 + 8 + 8 + 1) + 32,
     }.get(kernel, 32)

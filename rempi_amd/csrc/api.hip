@@ -119,6 +119,24 @@ hipError_t static_scratch_of(int device, unsigned char** out) {
 }
 }  // namespace
 
+// Gate of the kernels that keep every SIMD busy by themselves (the chain simulation, the
+// permutation rebuild): the contexts of a process on one device take turns with them.  Two of
+// these kernels side by side each run at half speed and leave at the same time, so lanes that
+// met in one of them once stay in step ever after -- all in their issue-bound kernels together,
+// then all in their bandwidth-bound ones, each resource idle while the other is the limit.
+// With one such kernel at a time the lanes spread out, and the other lanes' bandwidth-bound
+// kernels run beside it.  A context entering a gate makes its stream wait for the event the
+// previous holder recorded behind its kernel; the order is the order of the host calls, so
+// the waits cannot form a cycle.
+struct Gate {
+  std::mutex m;
+  hipEvent_t last = nullptr;
+  const void* owner = nullptr;
+};
+constexpr int kGateKinds = 2;    // 0: chain, 1: permutation rebuild
+constexpr int kGateDevices = 16;
+static Gate g_gates[kGateDevices][kGateKinds];
+
 struct cdcx_ctx {
   int device = 0;
   unsigned char* static_scratch = nullptr;  // this device's `scratch` (static_scratch_of)
@@ -184,6 +202,11 @@ struct cdcx_ctx {
   bool chain_g16 = getenv("CDCX_CHAIN_G16") != nullptr;  // first tier on 16-lane groups (A/B timing)
   // segments of at least this many events run at raised wave priority in the 8-lane chain tier
   int chain_long = getenv("CDCX_CHAIN_LONG") ? atoi(getenv("CDCX_CHAIN_LONG")) : 1536;
+  // gates in use: bit 0 chain, bit 1 permutation rebuild, bit 2 both kinds through one gate
+  // (off by default: on the bench batch the gates change the rate by less than 1 %)
+  int gate_mode = getenv("CDCX_GATE") ? atoi(getenv("CDCX_GATE")) : 0;
+  hipEvent_t gate_ev[kGateKinds][4] = {};
+  int gate_next[kGateKinds] = {};
   int64_t chain_tier_counts[3] = {0, 0, 0};  // segments entering each tier in the last encode
 
   template <class T>
@@ -252,6 +275,24 @@ struct cdcx_ctx {
       HIPCHK(hipEventRecord(e1, s));
       pending.push_back({kid, e0, e1});
     }
+  }
+  // launch() of a kernel that passes through gate `kind` (see Gate)
+  template <class K, class... Args>
+  void launch_gated(int kind, int kid, K kernel, dim3 g, dim3 b, hipStream_t s, Args... args) {
+    if (!((gate_mode >> kind) & 1) || device >= kGateDevices) {
+      launch(kid, kernel, g, b, s, args...);
+      return;
+    }
+    Gate& gt = g_gates[device][(gate_mode & 4) ? 0 : kind];
+    std::lock_guard<std::mutex> lk(gt.m);
+    if (gt.last && gt.owner != this) HIPCHK(hipStreamWaitEvent(s, gt.last, 0));
+    launch(kid, kernel, g, b, s, args...);
+    hipEvent_t& e = gate_ev[kind][gate_next[kind]];
+    gate_next[kind] = (gate_next[kind] + 1) & 3;
+    if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(e, s));
+    gt.last = e;
+    gt.owner = this;
   }
   void collect(hipStream_t s) {
     HIPCHK(hipStreamSynchronize(s));
@@ -617,7 +658,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
                   (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,
                   d_topg, d_qn, d_ovf1, d_cnt + 1, d_err);
       else
-        c->launch(K_CHAIN_G8, k_chain_grp8,
+        c->launch_gated(0, K_CHAIN_G8, k_chain_grp8,
                   dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(c->chain_grid, blocks(n, 128)))), dim3(256), s,
                   (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,
                   d_topg, d_qn, d_ovf1, d_cnt + 1, (int32_t)c->chain_long, d_err);
@@ -800,7 +841,7 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   HIPCHK(hipMemsetAsync(d_nfail, 0, 8, s));
   int32_t* d_order = c->buf<int32_t>("d_perm_order", NU);
   c->launch(K_LISTS, k_dec_order, dim3(blocks(NU, 256)), dim3(256), s, (const DUnit*)d_units, NU, d_order);
-  c->launch(K_DEC_WIN1, k_dec_perm_grp, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order, NU, d_in,
+  c->launch_gated(1, K_DEC_WIN1, k_dec_perm_grp, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order, NU, d_in,
             d_idd, d_dld, d_perm, d_cinv, d_nfail);
   // The record tiles are listed while the rebuild runs; the reconstruction itself is launched
   // before the wait for the failure count when no unit can have failed into a later tier.
@@ -1020,6 +1061,17 @@ void cdcx_destroy(cdcx_ctx* c) {
   if (c->pin_in.p) (void)hipHostFree(c->pin_in.p);
   if (c->pin_tab.p) (void)hipHostFree(c->pin_tab.p);
   if (c->pin_mail.p) (void)hipHostFree(c->pin_mail.p);
+  if (c->device < kGateDevices)
+    for (int k = 0; k < kGateKinds; k++) {
+      std::lock_guard<std::mutex> lk(g_gates[c->device][k].m);
+      if (g_gates[c->device][k].owner == c) {
+        g_gates[c->device][k].last = nullptr;
+        g_gates[c->device][k].owner = nullptr;
+      }
+    }
+  for (auto& ks : c->gate_ev)
+    for (auto e : ks)
+      if (e) (void)hipEventDestroy(e);
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   for (auto& p : c->pending) {
     (void)hipEventDestroy(p.a);
