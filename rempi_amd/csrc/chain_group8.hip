@@ -51,6 +51,8 @@ using mask64 = unsigned long long;
 __device__ __forceinline__ mask64 m_lt(int32_t x, int32_t y) { return __builtin_amdgcn_sicmp(x, y, 40); }
 __device__ __forceinline__ mask64 m_gt(int32_t x, int32_t y) { return __builtin_amdgcn_sicmp(x, y, 38); }
 __device__ __forceinline__ mask64 m_eq(int32_t x, int32_t y) { return __builtin_amdgcn_sicmp(x, y, 32); }
+__device__ __forceinline__ mask64 m_ne(int32_t x, int32_t y) { return __builtin_amdgcn_sicmp(x, y, 33); }
+__device__ __forceinline__ mask64 m_ge(int32_t x, int32_t y) { return __builtin_amdgcn_sicmp(x, y, 39); }
 // the group's byte of a lane mask (sh = the group's first lane)
 __device__ __forceinline__ uint32_t grp8(mask64 m, int sh) { return (uint32_t)(m >> sh) & 0xFFu; }
 
@@ -59,10 +61,11 @@ __device__ __forceinline__ int32_t first8(int32_t v) {
   int32_t t = __builtin_amdgcn_update_dpp(0, v, 0x150, 0xf, 0x3, false);  // row_newbcast:0 -> lanes 0-7 of the row
   return __builtin_amdgcn_update_dpp(t, v, 0x158, 0xf, 0xC, false);       // row_newbcast:8 -> lanes 8-15
 }
-// lane j <- lane j+1 (the group's lane 7 receives the neighbouring group's lane 0, or keeps its value)
-__device__ __forceinline__ int32_t next8(int32_t v) { return __builtin_amdgcn_update_dpp(v, v, 0x101, 0xf, 0xf, false); }
-// lane j <- lane j-1 (the group's lane 0 receives the neighbouring group's lane 7, or keeps its value)
-__device__ __forceinline__ int32_t prev8(int32_t v) { return __builtin_amdgcn_update_dpp(v, v, 0x111, 0xf, 0xf, false); }
+// lane j <- lane j+1 (the group's lane 7 receives the neighbouring group's lane 0, or 0: bound_ctrl, so
+// that the instruction needs no copy of the old value)
+__device__ __forceinline__ int32_t next8(int32_t v) { return __builtin_amdgcn_update_dpp(0, v, 0x101, 0xf, 0xf, true); }
+// lane j <- lane j-1 (the group's lane 0 receives the neighbouring group's lane 7, or 0)
+__device__ __forceinline__ int32_t prev8(int32_t v) { return __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true); }
 __device__ __forceinline__ uint32_t below(int j) { return (1u << j) - 1u; }
 
 // global accesses at a 32-bit byte offset from a wave-uniform base
@@ -231,27 +234,29 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
     }
 
     // ---- parent --------------------------------------------------------------------------
-    int32_t pv, pslot = 2 * G;  // pslot: the adopted leaf's slot, 16 = none
-    if (ks >= 1) {
-      G8_STAT(6);
-      const mask64 jn = m_lt(j, nl);
+    // Branches below are on wave-level masks (scalar branches); what differs between the
+    // groups of the wave is predicated, so no group's path leaves copies at a join.
+    int32_t pv;
+    uint32_t pslot;  // the adopted leaf's slot, 16 = none
+    {
+      const mask64 has = m_gt(ks, 0);  // groups with a level below the new node
+      const mask64 jn = m_lt(j, nl) & has;
       uint32_t eq = grp8(jn & m_eq(llv, ks) & m_lt(lcol, c), sh);
       uint32_t gt = grp8(jn & m_gt(llv, ks), sh);
       if (useB) {
-        const mask64 jnB = m_lt(j + G, nl);
+        const mask64 jnB = m_lt(j + G, nl) & has;
         eq |= grp8(jnB & m_eq(llvB, ks) & m_lt(lcolB, c), sh) << G;
         gt |= grp8(jnB & m_gt(llvB, ks), sh) << G;
       }
       const uint32_t wa = __builtin_ctz(eq | (1u << (2 * G)));  // first eligible level-k* leaf, 16 = none
       const uint32_t need = gt & below(wa);
-      uint32_t win = wa;
-      int32_t anc = -1;
-      bool interior = false;
-      if (need) {
+      uint32_t win = wa, ok = 0;
+      int32_t x = lid, xB = lidB;
+      if (m_ne((int32_t)need, 0) != 0) {
         G8_STAT(7);
         // every slot before wa holding a deeper leaf climbs to its level-k* ancestor at once
         const bool mine = (need >> j) & 1u;
-        int32_t x = lid, col = 0x7fffffff;
+        int32_t col = 0x7fffffff;
         if (mine) {
 #pragma unroll 1
           for (int32_t d = llv - ks; d > 0; d--) {
@@ -260,8 +265,7 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
           }
           col = ring_col(x);
         }
-        uint32_t ok = grp8(m_lt(col, c), sh);
-        int32_t xB = lidB;
+        ok = grp8(m_lt(col, c), sh);
         if (useB) {
           const bool mineB = (need >> (j + G)) & 1u;
           int32_t colB = 0x7fffffff;
@@ -272,43 +276,32 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
           }
           ok |= grp8(m_lt(colB, c), sh) << G;
         }
-        if (ok) {
-          G8_STAT(9);
-          win = __ffs(ok) - 1;
-          interior = true;
-          const int32_t ad = bp4 + ((win & 7) << 2);
-          anc = __builtin_amdgcn_ds_bpermute(ad, x);
-          if (useB) {
-            const int32_t aB = __builtin_amdgcn_ds_bpermute(ad, xB);
-            anc = win < G ? anc : aB;
-          }
+        win = ok ? (uint32_t)__ffs(ok) - 1u : wa;
+      }
+      const bool interior = ok != 0;  // the parent is an ancestor found by a climb, not a leaf
+      if ((m_ge((int32_t)win, 2 * G) & has) != 0) {
+        if (win >= 2 * G && ks > 0) raise_error(err, kErrCorrupt);  // cannot happen for a valid permutation
+      }
+      // the parent: slot win's ancestor (interior) or slot win's leaf itself, which is adopted
+      const int32_t ad = bp4 + ((win & 7) << 2);
+      pv = __builtin_amdgcn_ds_bpermute(ad, interior ? x : lid);
+      if (useB) {
+        const int32_t pB = __builtin_amdgcn_ds_bpermute(ad, interior ? xB : lidB);
+        pv = win < G ? pv : pB;
+      }
+      pslot = interior ? 2u * G : min(win, 2u * G);
+      if (m_lt(ks, 1) != 0) {  // some group's node is on level 1
+        const bool none = ks < 1, outside = none && ord != 0;
+        // first segment: level 1 hangs off the root; later segments: outside parent, resolved
+        // at stitching from (ordinal, first leaf) -- chain.hip
+        pv = none ? (ord == 0 ? -1 : -2 - nrel1) : pv;
+        if (__builtin_amdgcn_ballot_w64(outside) != 0) {
+          G8_STAT(11);
+          const int32_t f = first8(lid);
+          if (outside && j == 0) stg(exta, ab + 4u * (uint32_t)i, nl > 0 ? f : -1);
         }
+        nrel1 += outside ? 1 : 0;
       }
-      if (win >= 2 * G) {
-        raise_error(err, kErrCorrupt);  // cannot happen for a valid permutation
-        win = 0;
-      }
-      if (interior) {
-        pv = anc;
-      } else {
-        const int32_t ad = bp4 + ((win & 7) << 2);
-        pv = __builtin_amdgcn_ds_bpermute(ad, lid);
-        if (useB) {
-          const int32_t pB = __builtin_amdgcn_ds_bpermute(ad, lidB);
-          pv = win < G ? pv : pB;
-        }
-        pslot = win;
-      }
-    } else if (ord == 0) {
-      G8_STAT(10);
-      pv = -1;  // first segment: level 1 hangs off the root
-    } else {
-      // outside parent, resolved at stitching from (ordinal, first leaf) -- chain.hip
-      pv = -2 - nrel1;
-      G8_STAT(11);
-      const int32_t f = first8(lid);
-      if (j == 0) stg(exta, ab + 4u * (uint32_t)i, nl > 0 ? f : -1);
-      nrel1++;
     }
     pval = (j == t) ? pv : pval;
     if (j == 0) ring[i & (R - 1)] = make_int2(pv, c);
@@ -377,74 +370,73 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
       nl -= (pslot < 2 * G) ? 1 : 0;
     }
     // (the sweep comes before the append: the new node, on the open column itself, is never swept)
-    if (cv < 0) {
-      G8_STAT(15);
-      uint32_t dead = grp8(m_lt(j, nl) & m_lt(lcol, c), sh);
-      if (!useB) {
-        if (dead) {
-          G8_STAT(16);
-          const bool alive = j < nl && !((dead >> j) & 1u);
-          const int32_t dst = alive ? j - __popc(dead & below(j)) : G - 1;
-          const int32_t ad = bp4 + (dst << 2);
-          lid = __builtin_amdgcn_ds_permute(ad, lid);
-          llv = __builtin_amdgcn_ds_permute(ad, llv);
-          lcol = __builtin_amdgcn_ds_permute(ad, lcol);
-          nl -= __popc(dead);
-        }
-      } else {
-        dead |= grp8(m_lt(j + G, nl) & m_lt(lcolB, c), sh) << G;
-        if (dead) {
-          G8_STAT(17);
-          // compaction through LDS: slot s (alive) lands at s - #dead below it
-          const bool aliveA = j < nl && !((dead >> j) & 1u), aliveB = j + G < nl && !((dead >> (j + G)) & 1u);
-          if (aliveA) {
-            const int32_t d = j - __popc(dead & below(j));
-            comp[d] = lid;
-            comp[16 + d] = llv;
-            comp[32 + d] = lcol;
+    {
+      const mask64 sw = m_lt(cv, 0);  // groups whose row is on its first untaken column
+      if (sw != 0) {
+        G8_STAT(15);
+        uint32_t dead = grp8(sw & m_lt(j, nl) & m_lt(lcol, c), sh);
+        if (!useB) {
+          if (m_ne((int32_t)dead, 0) != 0) {
+            G8_STAT(16);
+            // (a group without dead leaves permutes its live slots onto themselves)
+            const bool alive = j < nl && !((dead >> j) & 1u);
+            const int32_t dst = alive ? j - __popc(dead & below(j)) : G - 1;
+            const int32_t ad = bp4 + (dst << 2);
+            lid = __builtin_amdgcn_ds_permute(ad, lid);
+            llv = __builtin_amdgcn_ds_permute(ad, llv);
+            lcol = __builtin_amdgcn_ds_permute(ad, lcol);
+            nl -= __popc(dead);
           }
-          if (aliveB) {
-            const int32_t d = j + G - __popc(dead & below(j + G));
-            comp[d] = lidB;
-            comp[16 + d] = llvB;
-            comp[32 + d] = lcolB;
+        } else {
+          dead |= grp8(sw & m_lt(j + G, nl) & m_lt(lcolB, c), sh) << G;
+          if (m_ne((int32_t)dead, 0) != 0) {
+            G8_STAT(17);
+            // compaction through LDS: slot s (alive) lands at s - #dead below it
+            const bool aliveA = j < nl && !((dead >> j) & 1u), aliveB = j + G < nl && !((dead >> (j + G)) & 1u);
+            if (aliveA) {
+              const int32_t d = j - __popc(dead & below(j));
+              comp[d] = lid;
+              comp[16 + d] = llv;
+              comp[32 + d] = lcol;
+            }
+            if (aliveB) {
+              const int32_t d = j + G - __popc(dead & below(j + G));
+              comp[d] = lidB;
+              comp[16 + d] = llvB;
+              comp[32 + d] = lcolB;
+            }
+            __builtin_amdgcn_wave_barrier();
+            lid = comp[j];
+            llv = comp[16 + j];
+            lcol = comp[32 + j];
+            lidB = comp[G + j];
+            llvB = comp[16 + G + j];
+            lcolB = comp[32 + G + j];
+            __builtin_amdgcn_wave_barrier();
+            nl -= __popc(dead);
           }
-          __builtin_amdgcn_wave_barrier();
-          lid = comp[j];
-          llv = comp[16 + j];
-          lcol = comp[32 + j];
-          lidB = comp[G + j];
-          llvB = comp[16 + G + j];
-          lcolB = comp[32 + G + j];
-          __builtin_amdgcn_wave_barrier();
-          nl -= __popc(dead);
         }
       }
     }
-    if (useB) {
-      if (nl == 2 * G) {  // leaf list outgrows the group: hand the segment to the next tier
+    if (m_ge(nl, G) != 0) {  // some group's list fills its A slots: the append goes to a B slot
+      const bool full = nl == 2 * G;
+      if (__builtin_amdgcn_ballot_w64(full) != 0) {  // leaf list outgrows the group: hand the segment to the next tier
         G8_STAT(18);
-        if (j == 0) ovf[atomicAdd(novf, 1)] = si;
-        si = -1;
-        s1 = i + 1;  // the rest of this iteration runs on junk state and ends the segment
-        nl = 0;
+        if (full && j == 0) ovf[atomicAdd(novf, 1)] = si;
+        si = full ? -1 : si;
+        s1 = full ? i + 1 : s1;  // the rest of this iteration runs on junk state and ends the segment
+        nl = full ? 0 : nl;
       }
-      if (j + G == nl) {
-        lidB = i;
-        llvB = k;
-        lcolB = c;
-      }
-    } else if (m_eq(nl, G) != 0) {  // a list filling its eighth slot appends to B slot 0
-      if (j + G == nl) {
-        lidB = i;
-        llvB = k;
-        lcolB = c;
-      }
+      const bool ap = j + G == nl;
+      lidB = ap ? i : lidB;
+      llvB = ap ? k : llvB;
+      lcolB = ap ? c : lcolB;
     }
-    if (j == nl) {
-      lid = i;
-      llv = k;
-      lcol = c;
+    {
+      const bool ap = j == nl;
+      lid = ap ? i : lid;
+      llv = ap ? k : llv;
+      lcol = ap ? c : lcol;
     }
     nl++;
     i++;
