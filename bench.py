@@ -335,12 +335,21 @@ def main():
     ws, rank, local = dist_env()
     import torch
 
+    # One process per GPU over RCCL.  CDCX_BENCH_BACKEND=gloo is the rehearsal of the N > 1 path
+    # on a box with fewer GPUs than processes: the processes share the GPUs round robin and the
+    # final reduction runs on host tensors.
+    backend = os.environ.get("CDCX_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if ws > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     import rempi_amd
     from rempi_amd import cdcx, shard
 
@@ -441,7 +450,8 @@ def main():
 
     counters, tmax = shard.reduce_counters(
         [n_records * args.steps, comp_bytes, ver["enc_ranks"], ver["enc_fail"], ver["dec_ranks"], ver["dec_fail"],
-         count if args.max_batches <= 0 else sum(n for _, n in plan)], elapsed, dist, "cuda")
+         count if args.max_batches <= 0 else sum(n for _, n in plan)], elapsed, dist,
+        "cuda" if backend == "nccl" else "cpu")
     total_records = counters[0]
     value = total_records * RECORD_BYTES / tmax / 1e9
     comp_per_event = counters[1] / max(total_records, 1)

@@ -130,8 +130,10 @@ hipError_t static_scratch_of(int device, unsigned char** out) {
 // the waits cannot form a cycle.
 struct Gate {
   std::mutex m;
-  hipEvent_t last = nullptr;
-  const void* owner = nullptr;
+  // the events behind the latest kernels that went through, newest last, and their contexts;
+  // a gate of depth d lets d kernels run side by side: a new one waits for the d-th newest
+  hipEvent_t last[4] = {nullptr, nullptr, nullptr, nullptr};
+  const void* owner[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 constexpr int kGateKinds = 2;    // 0: chain, 1: permutation rebuild
 constexpr int kGateDevices = 16;
@@ -203,8 +205,11 @@ struct cdcx_ctx {
   // segments of at least this many events run at raised wave priority in the 8-lane chain tier
   int chain_long = getenv("CDCX_CHAIN_LONG") ? atoi(getenv("CDCX_CHAIN_LONG")) : 1536;
   // gates in use: bit 0 chain, bit 1 permutation rebuild, bit 2 both kinds through one gate
-  // (off by default: on the bench batch the gates change the rate by less than 1 %)
-  int gate_mode = getenv("CDCX_GATE") ? atoi(getenv("CDCX_GATE")) : 0;
+  // (on the bench batch: + 1 % over 3 steps from a common start, + 2.7 % over 12 steps)
+  int gate_mode = getenv("CDCX_GATE") ? atoi(getenv("CDCX_GATE")) : 3;
+  // kernels of a kind allowed side by side (1 .. 4): {chain, permutation rebuild}
+  int gate_depth[kGateKinds] = {getenv("CDCX_GATE_CHAIN") ? atoi(getenv("CDCX_GATE_CHAIN")) : 1,
+                                getenv("CDCX_GATE_PERM") ? atoi(getenv("CDCX_GATE_PERM")) : 2};
   hipEvent_t gate_ev[kGateKinds][4] = {};
   int gate_next[kGateKinds] = {};
   int64_t chain_tier_counts[3] = {0, 0, 0};  // segments entering each tier in the last encode
@@ -284,15 +289,20 @@ struct cdcx_ctx {
       return;
     }
     Gate& gt = g_gates[device][(gate_mode & 4) ? 0 : kind];
+    const int depth = std::min(4, std::max(1, gate_depth[kind]));
     std::lock_guard<std::mutex> lk(gt.m);
-    if (gt.last && gt.owner != this) HIPCHK(hipStreamWaitEvent(s, gt.last, 0));
+    if (gt.last[4 - depth] && gt.owner[4 - depth] != this) HIPCHK(hipStreamWaitEvent(s, gt.last[4 - depth], 0));
     launch(kid, kernel, g, b, s, args...);
     hipEvent_t& e = gate_ev[kind][gate_next[kind]];
     gate_next[kind] = (gate_next[kind] + 1) & 3;
     if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventRecord(e, s));
-    gt.last = e;
-    gt.owner = this;
+    for (int q = 0; q < 3; q++) {
+      gt.last[q] = gt.last[q + 1];
+      gt.owner[q] = gt.owner[q + 1];
+    }
+    gt.last[3] = e;
+    gt.owner[3] = this;
   }
   void collect(hipStream_t s) {
     HIPCHK(hipStreamSynchronize(s));
@@ -1064,10 +1074,11 @@ void cdcx_destroy(cdcx_ctx* c) {
   if (c->device < kGateDevices)
     for (int k = 0; k < kGateKinds; k++) {
       std::lock_guard<std::mutex> lk(g_gates[c->device][k].m);
-      if (g_gates[c->device][k].owner == c) {
-        g_gates[c->device][k].last = nullptr;
-        g_gates[c->device][k].owner = nullptr;
-      }
+      for (int q = 0; q < 4; q++)
+        if (g_gates[c->device][k].owner[q] == c) {
+          g_gates[c->device][k].last[q] = nullptr;
+          g_gates[c->device][k].owner[q] = nullptr;
+        }
     }
   for (auto& ks : c->gate_ev)
     for (auto e : ks)
