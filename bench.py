@@ -243,6 +243,7 @@ class Lane:
 
 
 STAGGER_S = float(os.environ.get("CDCX_BENCH_STAGGER_MS", "0")) / 1e3  # experiment: lane k starts k * this later
+PROFILE_TIMED = os.environ.get("CDCX_BENCH_NOPROF", "0") == "0"  # experiment: HIP events around every kernel of the timed steps
 
 
 def run_lanes(lanes, fn, steps):
@@ -383,7 +384,7 @@ def main():
         run_lanes(active, Lane.step, args.warmup)
         for ln in active:
             ln.comp = 0
-            ln.ctx.set_profiling(True)
+            ln.ctx.set_profiling(PROFILE_TIMED)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         run_lanes(active, Lane.step, args.steps)
@@ -480,11 +481,15 @@ def main():
     else:
         per = {k: (v[0] / v[1], per_launch_records) for k, v in kern.items()}
     order = sorted(per, key=lambda k: -per[k][0])
-    dom = order[0]
-    dom_ms, dom_launches = kern.get(dom, (0.0, 0))
-    launch_ms, launch_records = per[dom]
-    dom_line = line(dom, launch_ms, launch_records)
-    top = [line(k, *per[k]) for k in order[:8]]
+    if order:
+        dom = order[0]
+        dom_ms, dom_launches = kern.get(dom, (0.0, 0))
+        launch_ms, launch_records = per[dom]
+        dom_line = line(dom, launch_ms, launch_records)
+        top = [line(k, *per[k]) for k in order[:8]]
+    else:  # no kernel was timed (no solo steps and no per-kernel events)
+        dom, dom_ms, dom_launches, launch_ms, top = None, 0.0, 0, 0.0, []
+        dom_line = {"achieved": None, "frac": None, "algorithmic_bytes_per_launch": None}
 
     if args.kernel_report and rank == 0:
         tot = sum(v[0] for v in kern.values())
