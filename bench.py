@@ -465,9 +465,12 @@ def main():
 
     def line(k, launch_ms, launch_records):
         algo = algorithmic_bytes(k, launch_records, comp_per_event)
-        ach = algo / (launch_ms / 1e3) / 1e9
-        d = {"kernel": k, "launch_ms": round(launch_ms, 3), "algorithmic_bytes_per_launch": round(algo),
-             "achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBS, 5)}
+        d = {"kernel": k, "launch_ms": round(launch_ms, 3), "algorithmic_bytes_per_launch": None, "achieved": None,
+             "frac": None}
+        if algo is not None:  # (kernels that touch a data-dependent part of the batch have no per-record figure)
+            ach = algo / (launch_ms / 1e3) / 1e9
+            d.update({"algorithmic_bytes_per_launch": round(algo), "achieved": round(ach, 2),
+                      "frac": round(ach / HBM_PEAK_GBS, 5)})
         pk = (traffic or {}).get("kernels", {}).get(k)
         if pk and pk.get("bytes_per_record") is not None:
             d["traffic"] = round(pk["bytes_per_record"] * launch_records)
@@ -584,7 +587,6 @@ def algorithmic_bytes(kernel, n_records, c):
         "k_epoch": m * 8,
         "k_chain_grp8": m * (4 + 4 + 4),
         "k_chain_grp16": m * (4 + 4 + 4),
-        "k_chain_grp64": m * (4 + 4 + 4),
         "k_chain_mark": m * (4 + 1),
         "k_positions": m * (4 + 1 + 4 + 1.4 + 4 + 1 + 4 + 1.4 + 1.64 * 8) / 2,  # mean of its two launches (rows, columns)
         "k_deltas": m * (1.3 * 4 + 0.64 * (4 + 4 + 4)),
@@ -592,8 +594,10 @@ def algorithmic_bytes(kernel, n_records, c):
                 "k_dec_sections": 0.3 * c,
         "k_dec_perm_grp": m * (0.64 * (8 + 16) + 8),
         "k_dec_records": c + m * (4 + 8 + 8 + 1) + 32,
-    }.get(kernel, 32)
-    return per * n_records
+        "k_chain_exits": m * 4 * 0.4,   # the parents on the paths from each segment's max-level rows to its first row
+        "k_cuts": m * (4 + 4),
+    }.get(kernel)
+    return None if per is None else per * n_records
 
 
 PMC_TRAFFIC = "profiles/r02/pmc_traffic.json"
