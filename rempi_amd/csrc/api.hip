@@ -524,7 +524,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   c->launch(K_UNITS_LB, k_units_lb, dim3(C), dim3(kMaxSets), s, (const Chunk*)d_chunks, C, (const int64_t*)d_lb_off,
             (const int32_t*)d_nsets, (const int32_t*)d_tstart, (const int64_t*)d_rec_off, (const int32_t*)d_t2s, d_lohi,
             d_ucnt, d_uw);
-  c->launch(K_LISTS, k_scan_chunks, dim3(1), dim3(1024), s, d_chunks, C, (const int32_t*)d_ucnt, (const int64_t*)d_uw,
+  c->launch(K_LISTS, k_scan_chunks, dim3(1), dim3(kScanBlock), s, d_chunks, C, (const int32_t*)d_ucnt, (const int64_t*)d_uw,
             (const int32_t*)d_cbase, R, d_ufirst, d_nunits, d_cw1, d_tot);
   c->launch(K_LISTS, k_fill_units, dim3(C), dim3(kMaxSets), s, (const Chunk*)d_chunks, (const int64_t*)d_lb_off,
             (const int2*)d_lohi, (const int32_t*)d_nsets, (const int32_t*)d_setlist, (const int64_t*)d_rec_off,
@@ -540,7 +540,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   // Clock-order rank: the windowed pass for every unit (tiles of kSortTile events); the units
   // it flags (wfail) are ranked again by the tile sort after the next wait, then get their
   // epoch line and cuts (both skip flagged units until then).
-  c->launch(K_LISTS, k_units_scan_prep, dim3(1), dim3(1024), s, d_units, (int32_t)c->rank_tier, d_tot);
+  c->launch(K_LISTS, k_units_scan_prep, dim3(1), dim3(kScanBlock), s, d_units, (int32_t)c->rank_tier, d_tot);
   const int64_t NSmax = N / kSortTile + lbn;  // >= sum of ceil(M / kSortTile)
   SortTile* d_st = c->buf<SortTile>("sort_tiles", NSmax);
   HIPCHK(hipMemsetAsync(d_st, 0xFF, (size_t)NSmax * sizeof(SortTile), s));  // unit -1: no tile
@@ -565,7 +565,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   // Wait 2 (again after the rare re-rank / big-epoch detours): totals and epoch sources per rank.
   auto totals = [&]() {
     HIPCHK(hipMemsetAsync(d_bound, 0, 8 * (size_t)R, s));
-    c->launch(K_LISTS, k_units_scan_cuts, dim3(1), dim3(1024), s, d_units, d_bound, d_tot);
+    c->launch(K_LISTS, k_units_scan_cuts, dim3(1), dim3(kScanBlock), s, d_units, d_bound, d_tot);
     Mail m(c, s, 64 + sizeof(EncTotals) + 8 * (size_t)R);
     const size_t o_err = m.add(d_err, 4), o_tot = m.add(d_tot, sizeof(EncTotals)), o_b = m.add(d_bound, 8 * (size_t)R);
     const uint8_t* h = m.wait();
@@ -732,7 +732,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int64_t* d_upre = c->buf<int64_t>("upre", (size_t)NU + 1);
   int64_t* d_cpre = c->buf<int64_t>("cpre", (size_t)C + 1);
   int64_t* d_files = c->buf<int64_t>("file_layout", 3 * (size_t)R + 1);  // file_off[R], file_len[R], foot_off[R], total
-  c->launch(K_LISTS, k_out_layout, dim3(1), dim3(1024), s, d_units, d_chunks, C, (const int32_t*)d_cbase, R,
+  c->launch(K_LISTS, k_out_layout, dim3(1), dim3(kScanBlock), s, d_units, d_chunks, C, (const int32_t*)d_cbase, R,
             (const int32_t*)d_fcount, (int32_t)c->rep, (const EncTotals*)d_tot, d_upre, d_cpre, d_files, d_files + R,
             d_files + 2 * R, d_files + 3 * R);
   c->launch(K_WRITE_UNITS, k_write_units, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_midx,
@@ -804,7 +804,7 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   HIPCHK(hipMemsetAsync(d_tot, 0, sizeof(DecTotals), s));
   c->launch(K_DEC_UNITS, k_dec_units, dim3(blocks(C, 64)), dim3(64), s, d_in, (const DChunk*)d_ch, C,
             (const int32_t*)nullptr, d_nu, (DUnit*)nullptr, d_err);
-  c->launch(K_LISTS, k_dec_scan_chunks, dim3(1), dim3(1024), s, (const int32_t*)d_nu, C, d_fu, d_tot);
+  c->launch(K_LISTS, k_dec_scan_chunks, dim3(1), dim3(kScanBlock), s, (const int32_t*)d_nu, C, d_fu, d_tot);
   DecTotals tot{};
   auto totals = [&]() {
     Mail m(c, s, 64 + sizeof(DecTotals));
@@ -820,7 +820,7 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   int32_t* d_rt0 = c->buf<int32_t>("d_rec_tile0", (size_t)NU + 1);
   c->launch(K_DEC_UNITS, k_dec_units, dim3(blocks(C, 64)), dim3(64), s, d_in, (const DChunk*)d_ch, C, (const int32_t*)d_fu,
             (int32_t*)nullptr, d_units, d_err);
-  c->launch(K_LISTS, k_dec_scan_units, dim3(1), dim3(1024), s, d_units, NU, (int32_t)std::min(std::max(c->dec_tier, 0), 2),
+  c->launch(K_LISTS, k_dec_scan_units, dim3(1), dim3(kScanBlock), s, d_units, NU, (int32_t)std::min(std::max(c->dec_tier, 0), 2),
             d_rt0, d_tot);
   totals();
   const int64_t wb = tot.rows, ro = tot.records, ko = tot.keys;

@@ -88,6 +88,11 @@ __device__ __host__ __forceinline__ uint64_t pack_key(int32_t clk, int32_t src) 
 __device__ __host__ __forceinline__ int32_t key_clock(uint64_t k) { return (int32_t)((uint32_t)(k >> 32) ^ 0x80000000u); }
 __device__ __host__ __forceinline__ int32_t key_source(uint64_t k) { return (int32_t)((uint32_t)k ^ 0x80000000u); }
 
+// For kernels of a few waves whose run time is a chain of dependent steps (scans over the unit
+// list, list walks): their waves issue ahead of the throughput kernels of other streams that
+// share the SIMD.  Without it a 70 us scan takes milliseconds while a chain kernel runs.
+__device__ __forceinline__ void latency_kernel() { __builtin_amdgcn_s_setprio(3); }
+
 // The same key as the two signed words {source, clock} (an int2 in memory): the form in which
 // a unit's keys are kept in clock order, at Unit::key_off, and handed to the replay side.
 constexpr uint64_t kKeyBias = 0x8000000080000000ull;

@@ -11,6 +11,8 @@
 
 namespace cdcx {
 
+constexpr int kScanBlock = 256;  // threads of the single-workgroup list scans (lists.hip)
+
 struct GenArgs {
   gen::Shape sh;
   int32_t first_rank;

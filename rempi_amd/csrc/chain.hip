@@ -105,6 +105,7 @@ constexpr int kLenBins = 4096;
 __device__ __forceinline__ int len_bin(int32_t len) { return kLenBins - 1 - min(len, kLenBins - 1); }
 
 __global__ void __launch_bounds__(256) k_seg_hist(const Seg* __restrict__ segs, int32_t nsegs, int32_t* __restrict__ hist) {
+  latency_kernel();
   __shared__ int32_t h[kLenBins];
   for (int q = threadIdx.x; q < kLenBins; q += 256) h[q] = 0;
   __syncthreads();
@@ -116,6 +117,7 @@ __global__ void __launch_bounds__(256) k_seg_hist(const Seg* __restrict__ segs, 
 }
 
 __global__ void __launch_bounds__(256) k_seg_bins(int32_t* __restrict__ hist) {
+  latency_kernel();
   __shared__ int32_t lds[4];
   int32_t run = 0;
   for (int b = 0; b < kLenBins; b += 256) {
@@ -129,6 +131,7 @@ __global__ void __launch_bounds__(256) k_seg_bins(int32_t* __restrict__ hist) {
 
 __global__ void __launch_bounds__(256) k_seg_order(const Seg* __restrict__ segs, int32_t nsegs, int32_t* __restrict__ hist,
                                                    int32_t* __restrict__ order) {
+  latency_kernel();
   __shared__ int32_t h[kLenBins];
   for (int q = threadIdx.x; q < kLenBins; q += 256) h[q] = 0;
   __syncthreads();
@@ -452,6 +455,7 @@ __global__ void __launch_bounds__(256) k_chain_exits(const Unit* __restrict__ un
                                                      int32_t nsegs, const int32_t* __restrict__ par,
                                                      const int32_t* __restrict__ exta, const int32_t* __restrict__ qn,
                                                      int32_t* __restrict__ qexit, uint32_t* err) {
+  latency_kernel();
   const int si = blockIdx.x * 256 + threadIdx.x;
   if (si >= nsegs) return;
   const Seg sg = segs[si];
@@ -464,6 +468,7 @@ __global__ void __launch_bounds__(256) k_chain_exits(const Unit* __restrict__ un
 // Per unit: chain entry index of every segment, last to first; chain length.
 __global__ void __launch_bounds__(64) k_chain_entries(Unit* __restrict__ units, int32_t n_units, Seg* __restrict__ segs,
                                                       const int32_t* __restrict__ qexit) {
+  latency_kernel();
   const int ui = blockIdx.x * 64 + threadIdx.x;
   if (ui >= n_units) return;
   Unit& u = units[ui];
@@ -488,6 +493,7 @@ __global__ void __launch_bounds__(64) k_chain_entries(Unit* __restrict__ units, 
 __global__ void __launch_bounds__(256) k_chain_mark(const Unit* __restrict__ units, const Seg* __restrict__ segs,
                                                     int32_t nsegs, const int32_t* __restrict__ par,
                                                     const int32_t* __restrict__ qn, uint8_t* __restrict__ chain) {
+  latency_kernel();
   const int32_t nw = gridDim.x * 4;
   const int l = lane_id();
   for (int32_t si = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wave_id()); si < nsegs; si += nw) {

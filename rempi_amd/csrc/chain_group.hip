@@ -90,6 +90,7 @@ __global__ void __launch_bounds__(256) k_chain_grp(const Unit* __restrict__ unit
   using Mask = typename Gr::Mask;
   constexpr int kGroups = 256 / G;
   constexpr int R = ring_rows<G>();
+  if (G == 64) latency_kernel();  // the second tier: a handful of segments, one per wave
   __shared__ int32_t next_j;
   __shared__ int2 ring_all[kGroups][R];  // {par, column} of row r at [r % R]
   int2* ring = ring_all[threadIdx.x / G];

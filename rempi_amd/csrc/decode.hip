@@ -17,6 +17,7 @@ namespace cdcx {
 __global__ void __launch_bounds__(64) k_dec_count_chunks(const uint8_t* __restrict__ in, const int64_t* __restrict__ off,
                                                          const int64_t* __restrict__ len, int32_t n_ranks,
                                                          int32_t* __restrict__ nchunks, uint32_t* err) {
+  latency_kernel();
   const int r = blockIdx.x * 64 + threadIdx.x;
   if (r >= n_ranks) return;
   const uint8_t* b = in + off[r];
@@ -43,6 +44,7 @@ __global__ void __launch_bounds__(64) k_dec_count_chunks(const uint8_t* __restri
 __global__ void __launch_bounds__(64) k_dec_list_chunks(const uint8_t* __restrict__ in, const int64_t* __restrict__ off,
                                                         const int32_t* __restrict__ cbase, const int32_t* __restrict__ nchunks,
                                                         int32_t n_ranks, DChunk* __restrict__ chunks) {
+  latency_kernel();
   const int r = blockIdx.x * 64 + threadIdx.x;
   if (r >= n_ranks) return;
   int64_t p = off[r];
@@ -120,6 +122,7 @@ __device__ bool walk_units(const uint8_t* __restrict__ in, const DChunk& c, int3
 __global__ void __launch_bounds__(64) k_dec_units(const uint8_t* __restrict__ in, const DChunk* __restrict__ chunks,
                                                   int32_t n_chunks, const int32_t* __restrict__ first_unit,
                                                   int32_t* __restrict__ nunits, DUnit* __restrict__ units, uint32_t* err) {
+  latency_kernel();
   const int c = blockIdx.x * 64 + threadIdx.x;
   if (c >= n_chunks) return;
   int32_t k = 0;
@@ -137,6 +140,7 @@ __global__ void __launch_bounds__(64) k_dec_chunk_units(const uint8_t* __restric
                                                         int64_t max_rows, int64_t perm_capacity,
                                                         int32_t* __restrict__ hdr, int32_t* __restrict__ order,
                                                         DUnit* __restrict__ units) {
+  latency_kernel();
   __shared__ int32_t nu_s;
   if (threadIdx.x == 0) {
     int32_t k = 0;

@@ -51,6 +51,7 @@ __global__ void __launch_bounds__(256) k_tile_hist(const int32_t* __restrict__ r
 // the order test_tables_map (a std::map) emits them in (rempi_encoder_cdc.cpp:785-800).
 __global__ void __launch_bounds__(kMaxSets) k_set_dense(const uint32_t* __restrict__ presence, int16_t* __restrict__ dense,
                                                         int32_t* __restrict__ setlist, int32_t* __restrict__ nsets) {
+  latency_kernel();
   const int r = blockIdx.x, sid = threadIdx.x;
   const uint32_t* p = presence + r * (kMaxSets / 32);
   const int w = sid >> 5, b = sid & 31;
@@ -69,6 +70,7 @@ __global__ void __launch_bounds__(256) k_hist_scan(const uint32_t* __restrict__ 
                                                    const int32_t* __restrict__ ntiles, const int32_t* __restrict__ nsets,
                                                    const int32_t* __restrict__ setlist, int32_t* __restrict__ base,
                                                    int32_t* __restrict__ tstart, uint8_t* __restrict__ prevm) {
+  latency_kernel();
   __shared__ int32_t lds[4];
   const int r = blockIdx.x;
   const int T = nsets[r], t0 = tile0[r], nt = ntiles[r];
@@ -205,6 +207,7 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
 __global__ void __launch_bounds__(256) k_rank_scan(const int32_t* __restrict__ tsum, const int32_t* __restrict__ tile0,
                                                    const int32_t* __restrict__ ntiles, int32_t* __restrict__ toff,
                                                    int32_t* __restrict__ rtot) {
+  latency_kernel();
   __shared__ int32_t lds[4];
   const int r = blockIdx.x;
   const int t0 = tile0[r], nt = ntiles[r];
@@ -235,6 +238,7 @@ __global__ void __launch_bounds__(64) k_chunks(const int32_t* __restrict__ rec, 
                                                const int32_t* __restrict__ tstart, const int32_t* __restrict__ nsets,
                                                const int64_t* __restrict__ ccap_off, int64_t max_len,
                                                int2* __restrict__ chunks, int32_t* __restrict__ nchunks) {
+  latency_kernel();
   const int r = blockIdx.x, l = lane_id();
   const int64_t rb = rec_off[r];
   const int32_t n = (int32_t)nrec[r];
@@ -336,6 +340,7 @@ __global__ void __launch_bounds__(kMaxSets) k_units_lb(const Chunk* __restrict__
                                                        const int32_t* __restrict__ tstart, const int64_t* __restrict__ rec_off,
                                                        const int32_t* __restrict__ t2s, int2* __restrict__ lohi,
                                                        int32_t* __restrict__ ucnt, int64_t* __restrict__ uw) {
+  latency_kernel();
   __shared__ int64_t lds[kMaxSets / kWave];
   const int c = blockIdx.x;
   if (c >= n_chunks) return;
@@ -1254,6 +1259,7 @@ __global__ void __launch_bounds__(256) k_write_units(const Unit* __restrict__ un
 }
 
 __global__ void __launch_bounds__(256) k_chunk_headers(const Chunk* __restrict__ ch, int32_t n, uint8_t* __restrict__ out) {
+  latency_kernel();
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < n) st_u64(out + ch[i].out_off, (uint64_t)ch[i].payload);
 }
@@ -1271,6 +1277,7 @@ __global__ void __launch_bounds__(256) k_footer_order(const Unit* __restrict__ u
                                                       const int64_t* __restrict__ fb_off, uint64_t* __restrict__ fkey,
                                                       int32_t* __restrict__ fnext, int32_t* __restrict__ fbucket,
                                                       int32_t* __restrict__ fcount) {
+  latency_kernel();
   constexpr int HC = 4096, LCAP = HC / 2;
   __shared__ int32_t hkey[HC];
   __shared__ unsigned long long hord[HC];
@@ -1369,6 +1376,7 @@ __global__ void __launch_bounds__(64) k_footer_write(const int64_t* __restrict__
                                                      const int32_t* __restrict__ fbucket, const int32_t* __restrict__ fcount,
                                                      const int64_t* __restrict__ foot_off, int32_t n_ranks,
                                                      uint8_t* __restrict__ out) {
+  latency_kernel();
   const int r = blockIdx.x * 64 + threadIdx.x;
   if (r >= n_ranks) return;
   uint8_t* o = out + foot_off[r];

@@ -5,9 +5,12 @@
 // the segment offsets (after k_cuts) and the output layout (after k_deltas and k_footer_order).
 // The replay side needs the unit offsets, the launch order of the permutation rebuild and the
 // record tiles.  Every one of them is a scan over a few thousand descriptors: a single
-// workgroup of 1024 threads does it in a few rounds, and the host only reads back the handful
+// workgroup does it in a few dozen rounds, and the host only reads back the handful
 // of totals that size buffers and grids (EncTotals / DecTotals) instead of downloading,
-// walking and re-uploading the descriptor arrays between kernels.
+// walking and re-uploading the descriptor arrays between kernels.  (256 threads, not 1024: a
+// workgroup needs all its wave slots on one CU, and while other streams' kernels fill the CUs
+// a 16-wave workgroup waited milliseconds for a CU with room -- the scans took 1.2-3.4 ms each
+// under load against 0.07 ms alone.)
 #include <hip/hip_runtime.h>
 
 #include "cdcx_device.h"
@@ -16,7 +19,6 @@
 namespace cdcx {
 
 namespace {
-constexpr int kScanBlock = 1024;
 
 // Exclusive scan of v over the block's threads plus a running carry; returns the exclusive
 // prefix including the carry and advances the carry by the round's total.
@@ -33,6 +35,7 @@ __device__ __forceinline__ T scan_round(T v, T& carry, T* lds) {
 // Record tiles of every rank: tile q of rank r covers records [q * kTile, ...) of the rank.
 __global__ void __launch_bounds__(256) k_build_tiles(const int64_t* __restrict__ rec_off, const int32_t* __restrict__ tile0,
                                                      Tile* __restrict__ tiles) {
+  latency_kernel();
   const int r = blockIdx.x;
   const int64_t b = rec_off[r], n = rec_off[r + 1] - b;
   for (int64_t q = threadIdx.x; q * kTile < n; q += 256)
@@ -45,6 +48,7 @@ __global__ void __launch_bounds__(256) k_build_chunks(const int2* __restrict__ c
                                                       const int32_t* __restrict__ nchunks, const int32_t* __restrict__ nsets,
                                                       const int32_t* __restrict__ cbase, const int64_t* __restrict__ lbase,
                                                       Chunk* __restrict__ chunks, int64_t* __restrict__ lb_off) {
+  latency_kernel();
   const int r = blockIdx.x;
   const int32_t n = nchunks[r], T = nsets[r];
   for (int32_t k = threadIdx.x; k < n; k += 256) {
@@ -62,6 +66,7 @@ __global__ void __launch_bounds__(kScanBlock) k_scan_chunks(Chunk* __restrict__ 
                                                             const int32_t* __restrict__ cbase, int32_t R,
                                                             int32_t* __restrict__ ufirst, int32_t* __restrict__ nunits,
                                                             int64_t* __restrict__ cw1, EncTotals* __restrict__ tot) {
+  latency_kernel();
   __shared__ int64_t lds[kScanBlock / kWave];
   int64_t cu = 0, cw = 0;
   for (int32_t b = 0; b < C; b += kScanBlock) {
@@ -93,6 +98,7 @@ __global__ void __launch_bounds__(kMaxSets) k_fill_units(const Chunk* __restrict
                                                          const int32_t* __restrict__ setlist,
                                                          const int64_t* __restrict__ rec_off, const int64_t* __restrict__ cw1,
                                                          Unit* __restrict__ units, int64_t* __restrict__ w1) {
+  latency_kernel();
   __shared__ int64_t lds[kMaxSets / kWave];
   const int32_t c = blockIdx.x;
   const Chunk C = chunks[c];
@@ -121,6 +127,7 @@ __global__ void __launch_bounds__(kMaxSets) k_fill_units(const Chunk* __restrict
 // flag (1 = take the tile sort), totals.
 __global__ void __launch_bounds__(kScanBlock) k_units_scan_prep(Unit* __restrict__ units, int32_t rank_tier,
                                                                 EncTotals* __restrict__ tot) {
+  latency_kernel();
   __shared__ int64_t lds[kScanBlock / kWave];
   const int32_t NU = tot->n_units;
   int64_t ct = 0, cm = 0, cw = 0, cr = 0;
@@ -147,6 +154,7 @@ __global__ void __launch_bounds__(kScanBlock) k_units_scan_prep(Unit* __restrict
 }
 
 __global__ void __launch_bounds__(256) k_fill_sort_tiles(const Unit* __restrict__ units, SortTile* __restrict__ st) {
+  latency_kernel();
   const Unit u = units[blockIdx.x];
   for (int32_t q = threadIdx.x; q * kSortTile < u.M; q += 256) st[u.sort_tile0 + q] = SortTile{(int32_t)blockIdx.x, q};
 }
@@ -156,6 +164,7 @@ __global__ void __launch_bounds__(256) k_fill_sort_tiles(const Unit* __restrict_
 // (bound[], zeroed by the host) and in total.
 __global__ void __launch_bounds__(kScanBlock) k_units_scan_cuts(Unit* __restrict__ units, int64_t* __restrict__ bound,
                                                                 EncTotals* __restrict__ tot) {
+  latency_kernel();
   __shared__ int64_t lds[kScanBlock / kWave];
   const int32_t NU = tot->n_units;
   int64_t cs = 0, cf = 0, cb = 0, ce = 0;
@@ -181,6 +190,7 @@ __global__ void __launch_bounds__(kScanBlock) k_units_scan_cuts(Unit* __restrict
 }
 
 __global__ void __launch_bounds__(256) k_units_clear_wfail(Unit* __restrict__ units, int32_t NU) {
+  latency_kernel();
   const int32_t u = blockIdx.x * 256 + threadIdx.x;
   if (u < NU) units[u].wfail = 0;
 }
@@ -196,6 +206,7 @@ __global__ void __launch_bounds__(kScanBlock) k_out_layout(Unit* __restrict__ un
                                                            int64_t* __restrict__ cpre, int64_t* __restrict__ file_off,
                                                            int64_t* __restrict__ file_len, int64_t* __restrict__ foot_off,
                                                            int64_t* __restrict__ total) {
+  latency_kernel();
   __shared__ int64_t lds[kScanBlock / kWave];
   const int32_t NU = tot->n_units;
   int64_t carry = 0;
@@ -254,6 +265,7 @@ __global__ void __launch_bounds__(kScanBlock) k_out_layout(Unit* __restrict__ un
 // First unit of every chunk from the per-chunk unit counts of k_dec_units' counting pass.
 __global__ void __launch_bounds__(kScanBlock) k_dec_scan_chunks(const int32_t* __restrict__ nu, int32_t C,
                                                                 int32_t* __restrict__ first_unit, DecTotals* __restrict__ tot) {
+  latency_kernel();
   __shared__ int64_t lds[kScanBlock / kWave];
   int64_t carry = 0;
   for (int32_t b = 0; b < C; b += kScanBlock) {
@@ -268,6 +280,7 @@ __global__ void __launch_bounds__(kScanBlock) k_dec_scan_chunks(const int32_t* _
 // permutation-rebuild tier, totals.
 __global__ void __launch_bounds__(kScanBlock) k_dec_scan_units(DUnit* __restrict__ units, int32_t NU, int32_t tier,
                                                                int32_t* __restrict__ tile0, DecTotals* __restrict__ tot) {
+  latency_kernel();
   __shared__ int64_t lds[kScanBlock / kWave];
   int64_t cw = 0, cr = 0, ck = 0, ct = 0;
   for (int32_t b = 0; b < NU; b += kScanBlock) {
@@ -302,6 +315,7 @@ __global__ void __launch_bounds__(kScanBlock) k_dec_scan_units(DUnit* __restrict
 // Launch order of the permutation rebuild: units by descending pair count, equal counts in file
 // order (a stable sort by counting: order[#units that come before q] = q).
 __global__ void __launch_bounds__(256) k_dec_order(const DUnit* __restrict__ units, int32_t NU, int32_t* __restrict__ order) {
+  latency_kernel();
   __shared__ int32_t tp[256];
   const int32_t q = blockIdx.x * 256 + threadIdx.x;
   const int32_t P = q < NU ? units[q].P : 0;
@@ -320,6 +334,7 @@ __global__ void __launch_bounds__(256) k_dec_order(const DUnit* __restrict__ uni
 // one tile for a unit that only holds unmatched runs).
 __global__ void __launch_bounds__(256) k_dec_fill_tiles(const DUnit* __restrict__ units, const int32_t* __restrict__ tile0,
                                                         int2* __restrict__ tiles) {
+  latency_kernel();
   const int32_t q = blockIdx.x;
   const int32_t t0 = tile0[q], n = tile0[q + 1] - t0;
   for (int32_t k = threadIdx.x; k < n; k += 256) tiles[t0 + k] = make_int2(q, k);
