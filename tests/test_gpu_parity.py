@@ -247,3 +247,29 @@ def test_rank_tiers_vs_oracle(tier, monkeypatch):
                 bad.append(("move", i, k, first_diff(got, want)))
     assert not bad, bad[:5]
     c.close()
+
+
+@pytest.mark.parametrize("reach", [12, 45, 300, 1500])
+def test_chain_deep_levels_vs_oracle(reach):
+    """Long rising runs with elements displaced up to `reach` places: new nodes land far below
+    the top level, so the chain kernel searches and updates the spilled tops -- the eight levels
+    in registers, the LDS ring of the last 32 spilled levels and the lines already written to
+    memory -- and the edit sequence has entries far from their column's stretch."""
+    rng = np.random.default_rng(1000 + reach)
+    c = ctx(131072)
+    bad = []
+    for t in range(6):
+        n = int(rng.integers(1500, 6000))
+        order = list(range(n))
+        for _ in range(n // 25):  # move 4 % of the elements up to `reach` places
+            i = int(rng.integers(0, n))
+            j = int(np.clip(i + rng.integers(-reach, reach + 1), 0, n - 1))
+            order.insert(j, order.pop(i))
+        recs = S.permutation_stream(order, src=3)
+        want, _ = O.encode(recs, 131072)
+        got = c.encode_stream(recs)
+        if got != want:
+            bad.append((t, n, first_diff(got, want)))
+        elif c.decode_stream(got) != O.decode(want):
+            bad.append((t, n, "tables"))
+    assert not bad, bad
