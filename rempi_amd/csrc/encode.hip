@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
           __popcll(peers) | ((1 | (int)(((mm >> (63 - __clzll((long long)peers))) & 1) << 1)) << 16);
   }
   __syncthreads();
-  {  // exclusive scan over (round, wave) for each table: thread = table
+  if ((int)threadIdx.x < T) {  // exclusive scan over (round, wave) for each table: thread = table
     const int tb = threadIdx.x;
     int32_t run = 0;
     int32_t pf = prevm[(int64_t)blockIdx.x * kMaxSets + tb];
@@ -177,6 +177,11 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
   __syncthreads();
   const int64_t rb = rec_off[t.rank];
   const int32_t spos0 = (int32_t)(t.start - rb);
+  // (block-uniform bases + unsigned 32-bit indices: scalar base plus vector offset addressing)
+  TRec* const trec_r = trec + rb;
+  int32_t* const t2s_r = t2s + rb;
+  const int32_t* const base_b = base + (int64_t)blockIdx.x * kMaxSets;
+  uint8_t* const inc_b = inc0s + (int64_t)blockIdx.x * kTile;
   int32_t sum = 0;
 #pragma unroll
   for (int j = 0; j < ROUNDS; j++) {
@@ -184,7 +189,7 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
     if (i >= t.len) continue;
     const int tb = my_t[j];
     const int32_t slot = wc[(j * 4 + w) * kMaxSets + tb];
-    const int32_t pos = base[(int64_t)blockIdx.x * kMaxSets + tb] + (slot & 0xffff) + my_rank[j];
+    const uint32_t pos = (uint32_t)(base_b[(uint32_t)tb] + (slot & 0xffff) + my_rank[j]);
     // lo = {count, type, flag, rank}, hi = {with_next, index, clock, set}
     TRec o;
     const bool matched = (lo[j].z == 1);
@@ -192,11 +197,11 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
     o.clk = hi[j].z;
     o.x = matched ? hi[j].y : lo[j].x;
     o.info = matched ? (0x80000000u | (hi[j].x != 0 ? 1u : 0u)) : 0u;
-    trec[rb + pos] = o;
-    t2s[rb + pos] = spos0 + i;
+    trec_r[pos] = o;
+    t2s_r[pos] = spos0 + i;
     const int prev = my_prev[j] ? my_prev[j] : (slot >> 16);
     const int32_t inc = (matched || prev != 1) ? 1 : 0;
-    inc0s[(int64_t)blockIdx.x * kTile + i] = (uint8_t)inc;
+    inc_b[(uint32_t)i] = (uint8_t)inc;
     sum += inc;
   }
   sum = block_sum<256>(sum, lds);
