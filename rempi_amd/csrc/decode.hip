@@ -555,9 +555,8 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
       // Common path without divergent branches: predicated selects, LDS accesses of
       // inactive lanes go to per-lane dummy slots; rare cases (slides, targets past the
       // window, rotations longer than 16 slots) take wave-uniform detours.
+      // (an id outside [0, M) has failed the unit when its batch was formed, in lp())
       const int32_t live = (k < P) ? 1 : 0;
-      const int32_t xbad = live & ((uint32_t)x >= (uint32_t)M ? 1 : 0);
-      failv |= xbad;
       int32_t act = live & (failv ^ 1);
       // an untouched x (at position x) is brought kGAhead slots before the window end
       const int32_t far = act & (x >= base + W ? 1 : 0);
@@ -623,6 +622,9 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
     }
     xs = (int32_t)xi;
     ds = (int32_t)xd;
+    // an id outside [0, M) among the batch's pairs fails the unit (for this tier) at once
+    const uint64_t badm = __builtin_amdgcn_ballot_w64(inb && (uint32_t)xs >= (uint32_t)M);
+    failv |= ((badm >> (threadIdx.x & 48)) & 0xffffu) ? 1 : 0;
   };
   auto steps = [&](int32_t k0) {
     const int32_t nq = min(16, Pmax - k0);
