@@ -631,8 +631,23 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
             (const int32_t*)d_ufirst, (const int32_t*)d_nunits, (const uint64_t*)d_ep_rank, R, (const int64_t*)d_fk_off,
             (const int64_t*)d_fb_off, d_fkey, d_fnext, d_fbucket, d_fcount);
 
-  int32_t* d_pid = nullptr;
-  int32_t* d_pdl = nullptr;
+  // Output layout on the device: as soon as the pair counts are known (after the chain), so
+  // that k_deltas writes the pair sections straight into the files.  The output buffer is
+  // sized for P = M in every unit (a few bytes per record more than the files take).
+  const int64_t total_max = 8ll * C + 72ll * NU + 16ll * tot.sources + foot_max +
+                            (c->rep ? 0 : 8ll * tot.with_next + 16ll * tot.matched + 16ll * tot.runs);
+  uint8_t* d_out = c->buf<uint8_t>("out", total_max);
+  // the units' clock-ordered keys, dense in file order since the rank pass: the replay side's key stream
+  int2* d_keys = reinterpret_cast<int2*>(d_skey);
+  int64_t* d_upre = c->buf<int64_t>("upre", (size_t)NU + 1);
+  int64_t* d_cpre = c->buf<int64_t>("cpre", (size_t)C + 1);
+  int64_t* d_files = c->buf<int64_t>("file_layout", 3 * (size_t)R + 1);  // file_off[R], file_len[R], foot_off[R], total
+  auto out_layout = [&] {
+    c->launch(K_LISTS, k_out_layout, dim3(1), dim3(kScanBlock), s, d_units, d_chunks, C, (const int32_t*)d_cbase, R,
+              (const int32_t*)d_fcount, (int32_t)c->rep, (const EncTotals*)d_tot, d_upre, d_cpre, d_files, d_files + R,
+              d_files + 2 * R, d_files + 3 * R);
+  };
+
   if (!c->rep) {  // the rep encoder writes no matched-event sections: no chain, no edit sequence
   Seg* d_segs = c->buf<Seg>("segs", nsegs);
   c->launch(K_SEG_LIST, k_seg_list, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_segend, d_segs);
@@ -708,6 +723,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
             (const int32_t*)d_qexit);
   c->launch(K_CHAIN_MARK, k_chain_mark, dim3((unsigned)std::min<int64_t>(8192, blocks(nsegs, 4))), dim3(256), s, (const Unit*)d_units,
             (const Seg*)d_segs, (int32_t)nsegs, (const int32_t*)d_par, (const int32_t*)d_qn, d_chain);
+  out_layout();  // (the pair counts are final: k_chain_entries)
   int32_t* d_posA = c->buf<int32_t>("posA", N);
   int32_t* d_crow = c->buf<int32_t>("crow", N);
   uint32_t* d_seq = c->buf<uint32_t>("seq", 2 * N);
@@ -716,28 +732,14 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
             (const uint8_t*)d_chain, d_posA, d_crow);
   c->launch(K_POSITIONS, k_pos_cols, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_inv,
             (const uint8_t*)d_chain, (const int32_t*)d_posA, (const int32_t*)d_crow, d_seq, d_sx);
-  d_pid = c->buf<int32_t>("pid", N);
-  d_pdl = c->buf<int32_t>("pdl", N);
   c->launch(K_DELTAS, k_deltas, dim3(NU), dim3(256), s, (const Unit*)d_units, (const uint32_t*)d_seq, (const int32_t*)d_sx,
-            d_pid, d_pdl);
+            d_out);
   }
 
-  // Output layout on the device.  The output buffer is sized before the pair counts are
-  // known, for P = M in every unit (a few bytes per record more than the files take).
-  const int64_t total_max = 8ll * C + 72ll * NU + 16ll * tot.sources + foot_max +
-                            (c->rep ? 0 : 8ll * tot.with_next + 16ll * tot.matched + 16ll * tot.runs);
-  uint8_t* d_out = c->buf<uint8_t>("out", total_max);
-  // the units' clock-ordered keys, dense in file order since the rank pass: the replay side's key stream
-  int2* d_keys = reinterpret_cast<int2*>(d_skey);
-  int64_t* d_upre = c->buf<int64_t>("upre", (size_t)NU + 1);
-  int64_t* d_cpre = c->buf<int64_t>("cpre", (size_t)C + 1);
-  int64_t* d_files = c->buf<int64_t>("file_layout", 3 * (size_t)R + 1);  // file_off[R], file_len[R], foot_off[R], total
-  c->launch(K_LISTS, k_out_layout, dim3(1), dim3(kScanBlock), s, d_units, d_chunks, C, (const int32_t*)d_cbase, R,
-            (const int32_t*)d_fcount, (int32_t)c->rep, (const EncTotals*)d_tot, d_upre, d_cpre, d_files, d_files + R,
-            d_files + 2 * R, d_files + 3 * R);
+  if (c->rep) out_layout();
   c->launch(K_WRITE_UNITS, k_write_units, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_midx,
             (const int32_t*)d_wp, (const int32_t*)d_run_id, (const uint64_t*)d_run_cnt, (const uint64_t*)d_ep_rank,
-            (const uint64_t*)d_ep_clk, (const int32_t*)d_pid, (const int32_t*)d_pdl, (int32_t)c->rep, d_out);
+            (const uint64_t*)d_ep_clk, (int32_t)c->rep, d_out);
   c->launch(K_CHUNK_HEADERS, k_chunk_headers, dim3(blocks(C, 256)), dim3(256), s, (const Chunk*)d_chunks, C, d_out);
   c->launch(K_FOOTER_WRITE, k_footer_write, dim3(blocks(R, 64)), dim3(64), s, (const int64_t*)d_fk_off,
             (const int64_t*)d_fb_off, (const uint64_t*)d_fkey, (const int32_t*)d_fnext, (const int32_t*)d_fbucket,

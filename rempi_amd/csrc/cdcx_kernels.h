@@ -63,9 +63,9 @@ __global__ void k_chain_mark(const Unit*, const Seg*, int32_t, const int32_t*, c
 __global__ void k_pos_rows(const Unit*, const int32_t*, const uint8_t*, int32_t*, int32_t*);
 __global__ void k_pos_cols(const Unit*, const int32_t*, const uint8_t*, const int32_t*, const int32_t*, uint32_t*,
                            int32_t*);
-__global__ void k_deltas(const Unit*, const uint32_t*, const int32_t*, int32_t*, int32_t*);
+__global__ void k_deltas(const Unit*, const uint32_t*, const int32_t*, uint8_t*);
 __global__ void k_write_units(const Unit*, const int32_t*, const int32_t*, const int32_t*, const uint64_t*,
-                              const uint64_t*, const uint64_t*, const int32_t*, const int32_t*, int32_t, uint8_t*);
+                              const uint64_t*, const uint64_t*, int32_t, uint8_t*);
 __global__ void k_chunk_headers(const Chunk*, int32_t, uint8_t*);
 __global__ void k_footer_order(const Unit*, const int32_t*, const int32_t*, const uint64_t*, int32_t, const int64_t*,
                                const int64_t*, uint64_t*, int32_t*, int32_t*, int32_t*);

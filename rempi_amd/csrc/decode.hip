@@ -556,28 +556,28 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
       // inactive lanes go to per-lane dummy slots; rare cases (slides, targets past the
       // window, rotations longer than 16 slots) take wave-uniform detours.
       // (an id outside [0, M) has failed the unit when its batch was formed, in lp())
-      const int32_t live = (k < P) ? 1 : 0;
-      int32_t act = live & (failv ^ 1);
+      // (flags of one step are lane masks; only the unit's failure is carried as a word)
+      bool act = (k < P) & (failv == 0);
       // an untouched x (at position x) is brought kGAhead slots before the window end
-      const int32_t far = act & (x >= base + W ? 1 : 0);
+      const bool far = act & (x >= base + W);
       if (__builtin_amdgcn_ballot_w64(far))
         while (__builtin_amdgcn_ballot_w64(far && x >= base + W - kGAhead)) slide(far && x >= base + W - kGAhead);
       const int2 e = emap[act ? (x & MM) : kGMap + j];
       int32_t p = e.y - base;
       int32_t t = p + d;
-      const int32_t bad = act & (((e.x != x) | ((uint32_t)p >= (uint32_t)W) | (t < 0) | (base + t > M - 1)) ? 1 : 0);
-      failv |= bad;
-      act &= bad ^ 1;
+      const bool bad = act & ((e.x != x) | ((uint32_t)p >= (uint32_t)W) | (t < 0) | (base + t > M - 1));
+      failv |= bad ? 1 : 0;
+      act &= !bad;
       if (__builtin_amdgcn_ballot_w64(act && t > W - 1)) {
         while (__builtin_amdgcn_ballot_w64(act && t > W - 1)) {
-          const int32_t go = act & (t > W - 1 ? 1 : 0);
-          const int32_t stuck = go & (p < 16 ? 1 : 0);
-          failv |= stuck;
-          act &= stuck ^ 1;
-          const int32_t sl = go & (stuck ^ 1);
-          slide(sl != 0);
-          p -= 16 * sl;
-          t -= 16 * sl;
+          const bool go = act & (t > W - 1);
+          const bool stuck = go & (p < 16);
+          failv |= stuck ? 1 : 0;
+          act &= !stuck;
+          const bool sl = go & !stuck;
+          slide(sl);
+          p -= sl ? 16 : 0;
+          t -= sl ? 16 : 0;
         }
       }
       // rotation of the slots between p and t, 16 at a time

@@ -1100,22 +1100,27 @@ __device__ __forceinline__ int32_t delta_word(uint32_t e) {
 }  // namespace
 
 __global__ void __launch_bounds__(256, 8) k_deltas(const Unit* __restrict__ units, const uint32_t* __restrict__ seq,
-                                                   const int32_t* __restrict__ sx, int32_t* __restrict__ pid,
-                                                   int32_t* __restrict__ pdl) {
+                                                   const int32_t* __restrict__ sx, uint8_t* __restrict__ out) {
   // LDS and registers are kept small (<= 20 KB, <= 64 VGPRs) so that 8 blocks share a CU.
   constexpr int32_t RING = 2048;  // the last RING sequence entries, for the span counts
   constexpr int32_t kLongSpan = 192;
   __shared__ int32_t lds[4];
   __shared__ int2 items[1024];  // second occurrences of the round: {position s, entry}, then {s, delta}
   __shared__ int32_t ring[RING];
-  __shared__ int32_t longs[1024];  // items of the round with long spans
+  __shared__ int32_t longs[1024];  // items of the round with long spans; then the ids of the round's pairs
   __shared__ int32_t nlong;
+  __shared__ int32_t carry[4];     // the last two ids and the last two deltas before this round (LP)
   const Unit u = units[blockIdx.x];
   const int64_t a = u.a;
   const uint32_t* sq = seq + 2 * a;
   const int32_t L = 2 * u.P + u.K;
   const int32_t* sxa = sx + 2 * a;
   int32_t ck = 0;
+  // The pairs go straight into the unit's pair section of the file, linear-predicted
+  // (compress_matched_events :706-721; x[i] - 2 x[i-1] + x[i-2] in 32 bits,
+  // rempi_compression_util.cpp:117-154): ids at the section start, deltas P words later.
+  uint8_t* const osec = out + u.out_off + 72 + 16ll * u.S + 8ll * u.W + 8ll * u.M + 16ll * u.U;
+  if (threadIdx.x < 4) carry[threadIdx.x] = 0;
   // this round's sequence entries; the next round's are loaded while the spans of this one
   // are counted
   uint32_t e[4];
@@ -1181,10 +1186,24 @@ __global__ void __launch_bounds__(256, 8) k_deltas(const Unit* __restrict__ unit
       if (lane_id() == 0) items[it].y = (((uint32_t)item.y & 3) == kRem) ? -d : d;
     }
     __syncthreads();
+    for (int32_t q = threadIdx.x; q < tot; q += 256) longs[q] = sxa[items[q].x];  // the pairs' ids
+    __syncthreads();
     for (int32_t q = threadIdx.x; q < tot; q += 256) {  // the round's pairs, coalesced
-      const int2 item = items[q];
-      pid[a + ck + q] = sxa[item.x];
-      pdl[a + ck + q] = item.y;
+      const uint32_t i0 = (uint32_t)longs[q], d0 = (uint32_t)items[q].y;
+      const uint32_t i1 = q >= 1 ? (uint32_t)longs[q - 1] : (uint32_t)carry[0];
+      const uint32_t d1 = q >= 1 ? (uint32_t)items[q - 1].y : (uint32_t)carry[2];
+      const uint32_t i2 = q >= 2 ? (uint32_t)longs[q - 2] : (uint32_t)carry[1 - q];
+      const uint32_t d2 = q >= 2 ? (uint32_t)items[q - 2].y : (uint32_t)carry[3 - q];
+      st_u32(osec + 4ll * (ck + q), i0 - 2 * i1 + i2);
+      st_u32(osec + 4ll * u.P + 4ll * (ck + q), d0 - 2 * d1 + d2);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && tot > 0) {
+      const int32_t pi = carry[0], pd = carry[2];
+      carry[1] = tot >= 2 ? longs[tot - 2] : pi;
+      carry[3] = tot >= 2 ? items[tot - 2].y : pd;
+      carry[0] = longs[tot - 1];
+      carry[2] = items[tot - 1].y;
     }
     ck += tot;
     __syncthreads();
@@ -1200,19 +1219,12 @@ __device__ __forceinline__ uint64_t lp64(const int32_t* x, int32_t i) {
   const uint64_t v2 = i >= 2 ? sext(x[i - 2]) : 0;
   return v0 - 2 * v1 + v2;
 }
-__device__ __forceinline__ uint32_t lp32(const int32_t* x, int32_t i) {
-  const uint32_t v0 = (uint32_t)x[i];
-  const uint32_t v1 = i >= 1 ? (uint32_t)x[i - 1] : 0;
-  const uint32_t v2 = i >= 2 ? (uint32_t)x[i - 2] : 0;
-  return v0 - 2 * v1 + v2;
-}
 
 __global__ void __launch_bounds__(256) k_write_units(const Unit* __restrict__ units, const int32_t* __restrict__ midx,
                                                      const int32_t* __restrict__ wp, const int32_t* __restrict__ run_id,
                                                      const uint64_t* __restrict__ run_cnt,
                                                      const uint64_t* __restrict__ ep_rank,
-                                                     const uint64_t* __restrict__ ep_clk, const int32_t* __restrict__ pid,
-                                                     const int32_t* __restrict__ pdl, int32_t rep,
+                                                     const uint64_t* __restrict__ ep_clk, int32_t rep,
                                                      uint8_t* __restrict__ out) {
   Unit u = units[blockIdx.x];
   const int64_t a = u.a;
@@ -1255,12 +1267,7 @@ __global__ void __launch_bounds__(256) k_write_units(const Unit* __restrict__ un
   p += 8;
   for (int i = t; i < u.U; i += 256) st_u64(p + 8 * i, run_cnt[a + i]);
   p += 8ull * u.U;
-  if (t == 0) st_u64(p, 8ull * u.P);
-  p += 8;
-  for (int i = t; i < u.P; i += 256) {
-    st_u32(p + 4 * i, lp32(pid + a, i));
-    st_u32(p + 4ull * u.P + 4 * i, lp32(pdl + a, i));
-  }
+  if (t == 0) st_u64(p, 8ull * u.P);  // (the pairs themselves: k_deltas)
 }
 
 __global__ void __launch_bounds__(256) k_chunk_headers(const Chunk* __restrict__ ch, int32_t n, uint8_t* __restrict__ out) {
