@@ -444,7 +444,7 @@ __global__ void __launch_bounds__(256) k_unit_prep(Unit* __restrict__ units, con
 // where "ordered before" is (key, index) order.  One pass, no sort: each tile of 1024 events
 // loads its events plus a halo of 2D + 1 before and D after, checks the condition for its
 // events (a key equal to the ~0 sentinel fails it too) and writes cord / inv / skey.  The cost
-// is linear in D, so every unit first tries D = 48 and only a unit with a failing tile repeats
+// is linear in D, so every unit first tries D = 40 and only a unit with a failing tile repeats
 // with D = kRankWin.  A unit that fails that too is flagged (Unit::wfail = 1); the host ranks
 // it again with the tile sort below, launched over the flagged units' tiles only.
 namespace {
@@ -549,7 +549,8 @@ __device__ __forceinline__ bool window_rank_tile(const Unit& u, int32_t tile, co
   for (int k = threadIdx.x; k < len; k += 256) cord[u.a + t0 + k] = rk[k];
   return bad;
 }
-constexpr int kRankNarrow = 48;
+// (the bench traces: the farthest pair out of clock order in a unit is 31-37 places apart)
+constexpr int kRankNarrow = 40;
 }  // namespace
 
 // First attempt, one block per tile, narrow window.  A remote violation can change the rank
