@@ -68,7 +68,8 @@ inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
 // Decode scratch lives in encode scratch that is dead by then (one context = one stream,
 // encode and decode never overlap): grow-only named buffers shared by both phases.
-constexpr const char* kAliasRecs = "trec";    // decoded records       <- T-order records
+constexpr const char* kAliasRecs = "dec_recs"; // decoded records: a buffer of their own (the T-order records keep the
+                                              // stream positions that cdcx_verify_roundtrip_device maps them by)
 constexpr const char* kAliasIdd = "mkey";     // pair ids              <- observed-order keys
 constexpr const char* kAliasDld = "seq";      // pair delays           <- edit sequence (the clock-order keys, "skey", are the decoder's input)
 constexpr const char* kAliasWpd = "run_cnt";  // with_previous         <- unmatched run counts
@@ -431,7 +432,8 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int64_t NT = 0;
   for (int r = 0; r < R; r++) {
     nrec[r] = rec_off[r + 1] - rec_off[r];
-    if (nrec[r] > INT32_MAX - 2) throw CdcxError{CDCX_ERR_LIMIT, "more than 2^31 records in one rank stream"};
+    // (a record's stream position travels in 30 bits of its T-order record)
+    if (nrec[r] > (int64_t)kInfoPos) throw CdcxError{CDCX_ERR_LIMIT, "more than 2^30 records in one rank stream"};
     tile0[r] = (int32_t)NT;
     ntiles[r] = (int32_t)((nrec[r] + kTile - 1) / kTile);
     NT += ntiles[r];
@@ -456,7 +458,6 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int32_t* d_tstart = c->buf<int32_t>("tstart", (size_t)R * (kMaxSets + 1));
   uint8_t* d_prevm = c->buf<uint8_t>("prevm", NT * kMaxSets);
   TRec* d_trec = c->buf<TRec>("trec", N);
-  int32_t* d_t2s = c->buf<int32_t>("t2s", N);
   uint8_t* d_inc0 = c->buf<uint8_t>("inc0s", NT * kTile);  // per tile: a rank's flags start kTile-aligned
   int32_t* d_tsum = c->buf<int32_t>("tsum", NT);
   int32_t* d_toff = c->buf<int32_t>("toff", NT);
@@ -473,13 +474,13 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
             (const int32_t*)d_ntiles, (const int32_t*)d_nsets, (const int32_t*)d_setlist, d_base, d_tstart, d_prevm);
   // (the scatter also forms the records' length increments and their tile sums)
   c->launch(K_SCATTER, k_scatter, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, (const int16_t*)d_dense,
-            (const int32_t*)d_base, (const uint8_t*)d_prevm, (const int32_t*)d_nsets, (const int64_t*)d_rec_off, d_trec, d_t2s,
+            (const int32_t*)d_base, (const uint8_t*)d_prevm, (const int32_t*)d_nsets, (const int64_t*)d_rec_off, d_trec,
             d_inc0, d_tsum);
   c->launch(K_RANK_SCAN, k_rank_scan, dim3(R), dim3(256), s, (const int32_t*)d_tsum, (const int32_t*)d_tile0,
             (const int32_t*)d_ntiles, d_toff, d_rtot);
   c->launch(K_CHUNKS, k_chunks, dim3(R), dim3(64), s, d_rec, (const int64_t*)d_rec_off, (const int64_t*)d_nrec,
             (const int32_t*)d_toff, (const int32_t*)d_rtot, (const int32_t*)d_tile0, (const uint8_t*)d_inc0,
-            (const int32_t*)d_t2s, (const int32_t*)d_tstart, (const int32_t*)d_nsets, (const int64_t*)d_ccap, maxl,
+            (const TRec*)d_trec, (const int32_t*)d_tstart, (const int32_t*)d_nsets, (const int64_t*)d_ccap, maxl,
             d_chunk_cap, d_nchunks);
 
   // Wait 1: tables and chunks per rank -> number of chunks and of (chunk, table) slots.
@@ -522,7 +523,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
             (const int32_t*)d_nchunks, (const int32_t*)d_nsets, (const int32_t*)d_cbase, (const int64_t*)d_lbase, d_chunks,
             d_lb_off);
   c->launch(K_UNITS_LB, k_units_lb, dim3(C), dim3(kMaxSets), s, (const Chunk*)d_chunks, C, (const int64_t*)d_lb_off,
-            (const int32_t*)d_nsets, (const int32_t*)d_tstart, (const int64_t*)d_rec_off, (const int32_t*)d_t2s, d_lohi,
+            (const int32_t*)d_nsets, (const int32_t*)d_tstart, (const int64_t*)d_rec_off, (const TRec*)d_trec, d_lohi,
             d_ucnt, d_uw);
   c->launch(K_LISTS, k_scan_chunks, dim3(1), dim3(kScanBlock), s, d_chunks, C, (const int32_t*)d_ucnt, (const int64_t*)d_uw,
             (const int32_t*)d_cbase, R, d_ufirst, d_nunits, d_cw1, d_tot);
@@ -1596,7 +1597,7 @@ int cdcx_verify_roundtrip_device(cdcx_ctx* c, const int32_t* d_rec, int64_t* mis
     unsigned long long* d_bad = c->buf<unsigned long long>("v_bad", 1);
     HIPCHK(hipMemsetAsync(d_bad, 0, 8, s));
     c->launch(K_VERIFY, k_verify_roundtrip, dim3(NU), dim3(256), s, (const Unit*)c->buf<Unit>("units", 0),
-              (const int64_t*)d_dec_off, (const int64_t*)d_rec_off, (const int32_t*)c->buf<int32_t>("t2s", 0),
+              (const int64_t*)d_dec_off, (const int64_t*)d_rec_off, (const TRec*)c->buf<TRec>("trec", 0),
               reinterpret_cast<const int4*>(d_rec), reinterpret_cast<const int4*>(c->d_rec_out), d_bad);
     *mismatches = (int64_t)c->download(d_bad, 1, s)[0];
   });

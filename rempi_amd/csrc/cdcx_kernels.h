@@ -26,13 +26,13 @@ __global__ void k_tile_hist(const int32_t*, const Tile*, uint32_t*, uint32_t*, u
 __global__ void k_hist_scan(const uint32_t*, const int32_t*, const int32_t*, const int32_t*, const int32_t*, int32_t*,
                             int32_t*, uint8_t*);
 __global__ void k_scatter(const int32_t*, const Tile*, const int16_t*, const int32_t*, const uint8_t*, const int32_t*,
-                          const int64_t*, TRec*, int32_t*, uint8_t*, int32_t*);
+                          const int64_t*, TRec*, uint8_t*, int32_t*);
 __global__ void k_rank_scan(const int32_t*, const int32_t*, const int32_t*, int32_t*, int32_t*);
 __global__ void k_chunks(const int32_t*, const int64_t*, const int64_t*, const int32_t*, const int32_t*, const int32_t*,
-                         const uint8_t*, const int32_t*, const int32_t*, const int32_t*, const int64_t*, int64_t, int2*,
+                         const uint8_t*, const TRec*, const int32_t*, const int32_t*, const int64_t*, int64_t, int2*,
                          int32_t*);
 __global__ void k_units_lb(const Chunk*, int32_t, const int64_t*, const int32_t*, const int32_t*, const int64_t*,
-                           const int32_t*, int2*, int32_t*, int64_t*);
+                           const TRec*, int2*, int32_t*, int64_t*);
 __global__ void k_unit_prep(Unit*, const TRec*, uint64_t*, int32_t*, int32_t*, int32_t*, uint64_t*, uint32_t*);
 __global__ void k_window_rank(Unit*, const SortTile*, const uint64_t*, int32_t*, int32_t*, uint64_t*);
 __global__ void k_window_rank_wide(Unit*, const uint64_t*, int32_t*, int32_t*, uint64_t*);
@@ -106,7 +106,7 @@ template <int K>
 __global__ void k_dec_perm_window(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
 __global__ void k_dec_records(const DUnit*, const int2*, const uint8_t*, const int32_t*, const uint8_t*, const uint64_t*,
                               const int2*, int4*);
-__global__ void k_verify_roundtrip(const Unit*, const int64_t*, const int64_t*, const int32_t*, const int4*, const int4*,
+__global__ void k_verify_roundtrip(const Unit*, const int64_t*, const int64_t*, const TRec*, const int4*, const int4*,
                                    unsigned long long*);
 __global__ void k_dec_pack_tables(const DUnit*, const int64_t*, const uint64_t*, const uint64_t*, const uint64_t*,
                                   const uint64_t*, uint64_t*);

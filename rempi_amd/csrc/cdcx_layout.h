@@ -30,14 +30,16 @@ struct Tile {
   int32_t pad;
 };
 
-// T-order compact record: {src, clock, index-or-count, info}; info bit31 = matched,
-// bit0 = with_next (matched only).  For unmatched records `x` holds event_count.
+// T-order compact record: {src, clock, index-or-count, info}; info bit 31 = matched, bit 30 =
+// with_next (matched only), bits 0-29 = the record's stream position in its rank (a rank trace
+// holds fewer than 2^30 records).  For unmatched records `x` holds event_count.
 struct TRec {
   int32_t src;
   int32_t clk;
   int32_t x;
   uint32_t info;
 };
+constexpr uint32_t kInfoMatched = 0x80000000u, kInfoWithNext = 0x40000000u, kInfoPos = 0x3fffffffu;
 
 struct Chunk {
   int32_t rank;

@@ -757,14 +757,14 @@ __global__ void __launch_bounds__(256) k_dec_records(const DUnit* __restrict__ u
 // (M + U == n for every unit); the host checks that before launching.
 __global__ void __launch_bounds__(256) k_verify_roundtrip(const Unit* __restrict__ units, const int64_t* __restrict__ dec_off,
                                                           const int64_t* __restrict__ rec_off,
-                                                          const int32_t* __restrict__ t2s, const int4* __restrict__ rec_in,
+                                                          const TRec* __restrict__ trec, const int4* __restrict__ rec_in,
                                                           const int4* __restrict__ rec_out,
                                                           unsigned long long* __restrict__ bad) {
   const Unit u = units[blockIdx.x];
   const int64_t rb = rec_off[u.rank], ob = dec_off[blockIdx.x];
   int32_t nbad = 0;
   for (int32_t i = threadIdx.x; i < u.n; i += 256) {
-    const int64_t g = rb + t2s[u.a + i];
+    const int64_t g = rb + (int64_t)(trec[u.a + i].info & kInfoPos);
     const int4 lo = rec_in[2 * g], hi = rec_in[2 * g + 1];
     const int4 a = rec_out[2 * (ob + i)], b = rec_out[2 * (ob + i) + 1];
     const bool m = lo.z == 1;

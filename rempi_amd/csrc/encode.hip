@@ -109,16 +109,17 @@ __global__ void __launch_bounds__(256) k_hist_scan(const uint32_t* __restrict__ 
 // previous record of the table is a lower lane of the wave, or the last one of an earlier
 // (round, wave) slot of the tile (carried through the slot scan), or the last one before the
 // tile (prevm).  inc0s is laid out per tile (tile * kTile + index), so a rank's flags are
-// contiguous from a kTile-aligned start; tsum = the tile's sum.
+// contiguous from a kTile-aligned start; tsum = the tile's sum.  A record's stream position
+// travels in its T-order record (TRec::info), which the chunk and unit searches read.
 __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
                                                  const int16_t* __restrict__ dense, const int32_t* __restrict__ base,
                                                  const uint8_t* __restrict__ prevm, const int32_t* __restrict__ nsets,
                                                  const int64_t* __restrict__ rec_off, TRec* __restrict__ trec,
-                                                 int32_t* __restrict__ t2s, uint8_t* __restrict__ inc0s,
-                                                 int32_t* __restrict__ tsum) {
+                                                 uint8_t* __restrict__ inc0s, int32_t* __restrict__ tsum) {
   constexpr int ROUNDS = kTile / 256;
   __shared__ int32_t wc[ROUNDS * 4 * kMaxSets];  // [round][wave][table]: count | last record's flags << 16
   __shared__ int32_t lds[4];
+  __shared__ uint8_t incs[kTile];  // the tile's flags, gathered so that a thread stores four consecutive ones
   for (int i = threadIdx.x; i < ROUNDS * 4 * kMaxSets; i += 256) wc[i] = 0;
   const Tile t = tiles[blockIdx.x];
   const int w = wave_id(), l = lane_id();
@@ -179,9 +180,7 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
   const int32_t spos0 = (int32_t)(t.start - rb);
   // (block-uniform bases + unsigned 32-bit indices: scalar base plus vector offset addressing)
   TRec* const trec_r = trec + rb;
-  int32_t* const t2s_r = t2s + rb;
   const int32_t* const base_b = base + (int64_t)blockIdx.x * kMaxSets;
-  uint8_t* const inc_b = inc0s + (int64_t)blockIdx.x * kTile;
   int32_t sum = 0;
 #pragma unroll
   for (int j = 0; j < ROUNDS; j++) {
@@ -196,16 +195,18 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
     o.src = lo[j].w;
     o.clk = hi[j].z;
     o.x = matched ? hi[j].y : lo[j].x;
-    o.info = matched ? (0x80000000u | (hi[j].x != 0 ? 1u : 0u)) : 0u;
+    o.info = (matched ? (kInfoMatched | (hi[j].x != 0 ? kInfoWithNext : 0u)) : 0u) | (uint32_t)(spos0 + i);
     trec_r[pos] = o;
-    t2s_r[pos] = spos0 + i;
     const int prev = my_prev[j] ? my_prev[j] : (slot >> 16);
     const int32_t inc = (matched || prev != 1) ? 1 : 0;
-    inc_b[(uint32_t)i] = (uint8_t)inc;
+    incs[i] = (uint8_t)inc;
     sum += inc;
   }
-  sum = block_sum<256>(sum, lds);
+  sum = block_sum<256>(sum, lds);  // (barriers: incs is complete)
   if (threadIdx.x == 0) tsum[blockIdx.x] = sum;
+  // (flags past the tile's length are never read)
+  reinterpret_cast<uint32_t*>(inc0s + (int64_t)blockIdx.x * kTile)[threadIdx.x] =
+      reinterpret_cast<const uint32_t*>(incs)[threadIdx.x];
 }
 
 // Per rank: exclusive scan of the tile sums of inc0 (toff) and their total (rtot).
@@ -239,7 +240,7 @@ __global__ void __launch_bounds__(256) k_rank_scan(const int32_t* __restrict__ t
 __global__ void __launch_bounds__(64) k_chunks(const int32_t* __restrict__ rec, const int64_t* __restrict__ rec_off,
                                                const int64_t* __restrict__ nrec, const int32_t* __restrict__ toff,
                                                const int32_t* __restrict__ rtot, const int32_t* __restrict__ tile0,
-                                               const uint8_t* __restrict__ inc0s, const int32_t* __restrict__ t2s,
+                                               const uint8_t* __restrict__ inc0s, const TRec* __restrict__ trec,
                                                const int32_t* __restrict__ tstart, const int32_t* __restrict__ nsets,
                                                const int64_t* __restrict__ ccap_off, int64_t max_len,
                                                int2* __restrict__ chunks, int32_t* __restrict__ nchunks) {
@@ -285,10 +286,10 @@ __global__ void __launch_bounds__(64) k_chunks(const int32_t* __restrict__ rec, 
         int32_t lo = ts[tb], hi = ts[tb + 1];
         while (lo < hi) {
           int32_t mid = (lo + hi) >> 1;
-          if (t2s[rb + mid] < s) lo = mid + 1; else hi = mid;
+          if ((int32_t)(trec[rb + mid].info & kInfoPos) < s) lo = mid + 1; else hi = mid;
         }
         if (lo < ts[tb + 1]) {
-          int32_t f = t2s[rb + lo];
+          int32_t f = (int32_t)(trec[rb + lo].info & kInfoPos);
           if (ib[f] == 0) corr[q] = f;
         }
       }
@@ -343,7 +344,7 @@ __global__ void __launch_bounds__(64) k_chunks(const int32_t* __restrict__ rec, 
 __global__ void __launch_bounds__(kMaxSets) k_units_lb(const Chunk* __restrict__ ch, int32_t n_chunks,
                                                        const int64_t* __restrict__ lb_off, const int32_t* __restrict__ nsets,
                                                        const int32_t* __restrict__ tstart, const int64_t* __restrict__ rec_off,
-                                                       const int32_t* __restrict__ t2s, int2* __restrict__ lohi,
+                                                       const TRec* __restrict__ trec, int2* __restrict__ lohi,
                                                        int32_t* __restrict__ ucnt, int64_t* __restrict__ uw) {
   latency_kernel();
   __shared__ int64_t lds[kMaxSets / kWave];
@@ -361,7 +362,7 @@ __global__ void __launch_bounds__(kMaxSets) k_units_lb(const Chunk* __restrict__
       int32_t lo = r0, hi = r1;
       while (lo < hi) {
         int32_t mid = (lo + hi) >> 1;
-        if (t2s[rb + mid] < x) lo = mid + 1; else hi = mid;
+        if ((int32_t)(trec[rb + mid].info & kInfoPos) < x) lo = mid + 1; else hi = mid;
       }
       return lo;
     };
@@ -397,7 +398,7 @@ __global__ void __launch_bounds__(256) k_unit_prep(Unit* __restrict__ units, con
     const bool valid = k < n;
     const TRec r = valid ? trec[a + k] : TRec{0, 0, 0, 0};
     const bool m = valid && (r.info >> 31);
-    const bool wn = m && (r.info & 1);
+    const bool wn = m && (r.info & kInfoWithNext);
     const bool rs = valid && !m && ((k == 0) || (trec[a + k - 1].info >> 31));
     uint64_t tot;
     const uint64_t ex =
