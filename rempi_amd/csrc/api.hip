@@ -283,9 +283,11 @@ struct cdcx_ctx {
     }
   }
   // launch() of a kernel that passes through gate `kind` (see Gate)
+  // `big`: only launches that fill the GPU take turns; a small one (a replay batch of a few
+  // hundred tables is bound by latency, not by issue) would only wait.
   template <class K, class... Args>
-  void launch_gated(int kind, int kid, K kernel, dim3 g, dim3 b, hipStream_t s, Args... args) {
-    if (!((gate_mode >> kind) & 1) || device >= kGateDevices) {
+  void launch_gated(int kind, bool big, int kid, K kernel, dim3 g, dim3 b, hipStream_t s, Args... args) {
+    if (!big || !((gate_mode >> kind) & 1) || device >= kGateDevices) {
       launch(kid, kernel, g, b, s, args...);
       return;
     }
@@ -684,7 +686,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
                   (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,
                   d_topg, d_qn, d_ovf1, d_cnt + 1, d_err);
       else
-        c->launch_gated(0, K_CHAIN_G8, k_chain_grp8,
+        c->launch_gated(0, n >= 65536, K_CHAIN_G8, k_chain_grp8,
                   dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(c->chain_grid, blocks(n, 128)))), dim3(256), s,
                   (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,
                   d_topg, d_qn, d_ovf1, d_cnt + 1, (int32_t)c->chain_long, d_err);
@@ -854,7 +856,7 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   HIPCHK(hipMemsetAsync(d_nfail, 0, 8, s));
   int32_t* d_order = c->buf<int32_t>("d_perm_order", NU);
   c->launch(K_LISTS, k_dec_order, dim3(blocks(NU, 256)), dim3(256), s, (const DUnit*)d_units, NU, d_order);
-  c->launch_gated(1, K_DEC_WIN1, k_dec_perm_grp, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order, NU, d_in,
+  c->launch_gated(1, NU >= 4096, K_DEC_WIN1, k_dec_perm_grp, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order, NU, d_in,
             d_idd, d_dld, d_perm, d_cinv, d_nfail);
   // The record tiles are listed while the rebuild runs; the reconstruction itself is launched
   // before the wait for the failure count when no unit can have failed into a later tier.
