@@ -1101,9 +1101,9 @@ __device__ __forceinline__ int32_t delta_word(uint32_t e) {
 }
 }  // namespace
 
-__global__ void __launch_bounds__(256, 8) k_deltas(const Unit* __restrict__ units, const uint32_t* __restrict__ seq,
+__global__ void __launch_bounds__(256, 7) k_deltas(const Unit* __restrict__ units, const uint32_t* __restrict__ seq,
                                                    const int32_t* __restrict__ sx, uint8_t* __restrict__ out) {
-  // LDS and registers are kept small (<= 20 KB, <= 64 VGPRs) so that 8 blocks share a CU.
+  // LDS and registers are kept small (20.5 KB, <= 72 VGPRs) so that 7 blocks share a CU.
   constexpr int32_t RING = 2048;  // the last RING sequence entries, for the span counts
   constexpr int32_t kLongSpan = 192;
   __shared__ int32_t lds[4];
