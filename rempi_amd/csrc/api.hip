@@ -719,9 +719,9 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     c->chain_tier_counts[2] = n;
   }
   int32_t* d_qexit = c->buf<int32_t>("qexit", N);
-  c->launch(K_CHAIN_EXITS, k_chain_exits, dim3(blocks(nsegs, 256)), dim3(256), s, (const Unit*)d_units,
-            (const Seg*)d_segs, (int32_t)nsegs, (const int32_t*)d_par, (const int32_t*)d_exta, (const int32_t*)d_qn,
-            d_qexit, d_err);
+  c->launch(K_CHAIN_EXITS, k_chain_exits, dim3((unsigned)std::min<int64_t>(8192, blocks(nsegs, 256))), dim3(256), s,
+            (const Unit*)d_units, (const Seg*)d_segs, (int32_t)nsegs, (const int32_t*)d_par, (const int32_t*)d_exta,
+            (const int32_t*)d_qn, d_qexit, d_err);
   c->launch(K_CHAIN_ENTRIES, k_chain_entries, dim3(blocks(NU, 64)), dim3(64), s, d_units, NU, d_segs,
             (const int32_t*)d_qexit);
   c->launch(K_CHAIN_MARK, k_chain_mark, dim3((unsigned)std::min<int64_t>(8192, blocks(nsegs, 4))), dim3(256), s, (const Unit*)d_units,

@@ -332,7 +332,7 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
     } else {
       // Outside parent: resolved at stitching from (ordinal, anchor of the first leaf).
       par[a + i] = -2 - nrel1;
-      // the first leaf; seg_exit climbs from it to its relative-level-1 ancestor
+      // the first leaf; k_chain_exits climbs from it to its relative-level-1 ancestor
       exta[a + i] = nl > 0 ? (slow ? leafg[lbase].x : lid[0]) : -1;
       nrel1++;
     }
@@ -431,38 +431,98 @@ template __global__ void k_chain_seg<16>(const Unit*, Seg*, int32_t, const int32
 // node; its outside parent is Q[j] of segment s-1 where j is its ordinal, or, when j >= |Q|,
 // that of its anchor -- the relative-level-1 ancestor of the segment's first leaf when the
 // node was created (exta holds that leaf) -- repeatedly.
-__device__ __forceinline__ int32_t seg_exit(const int32_t* __restrict__ par, const int32_t* __restrict__ exta,
-                                            int64_t a, int32_t v, int32_t qprev, uint32_t* err) {
-  int32_t guard = 0;
-  while (true) {
-    int32_t p = par[a + v];
-    while (p >= 0) {
-      v = p;
-      p = par[a + v];
-    }
-    const int32_t j = -2 - p;
-    if (j < qprev) return j;
-    v = exta[a + v];
-    if (v < 0 || ++guard > (1 << 28)) {
-      raise_error(err, kErrCorrupt);
-      return 0;
-    }
-  }
-}
-
-// Where the chain leaves segment s (ord > 0) for each of its max-level nodes.
+// Where the chain leaves segment s (ord > 0) for each of its max-level nodes: one wave per
+// segment, grid-stride.  Every step of the walk (a node's parent, or a relative-level-1 node's
+// anchor) leads to a lower row, so the walk is one sweep over the segment's rows from the top,
+// 64 rows (a chunk) at a time and four chunks per memory round trip; a single thread doing it
+// load by load pays a round trip per step, 250 steps for the average segment of a dense
+// table.  In a chunk each lane holds the next step of its row; pointer doubling over
+// ds_bpermute (at most six rounds) turns that into the first step that leaves the chunk, and
+// the walkers -- one lane per max-level node -- standing in the chunk take it.
 __global__ void __launch_bounds__(256) k_chain_exits(const Unit* __restrict__ units, const Seg* __restrict__ segs,
                                                      int32_t nsegs, const int32_t* __restrict__ par,
                                                      const int32_t* __restrict__ exta, const int32_t* __restrict__ qn,
                                                      int32_t* __restrict__ qexit, uint32_t* err) {
   latency_kernel();
-  const int si = blockIdx.x * 256 + threadIdx.x;
-  if (si >= nsegs) return;
-  const Seg sg = segs[si];
-  if (sg.ord == 0) return;
-  const int64_t a = units[sg.unit].a;
-  const int32_t qprev = segs[si - 1].qcount;
-  for (int32_t j = 0; j < sg.qcount; j++) qexit[a + sg.start + j] = seg_exit(par, exta, a, qn[a + sg.start + j], qprev, err);
+  const int l = lane_id();
+  const int32_t nw = gridDim.x * 4;
+  const int32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wave_id());
+  // the wave's segments w, w + nw, ...: 64 descriptions fetched side by side, one per lane
+  for (int64_t first = w; first < nsegs; first += (int64_t)64 * nw) {
+    const int64_t si = first + (int64_t)l * nw;
+    Seg sg = {};
+    if (si < nsegs) sg = segs[si];
+    const bool live = sg.ord != 0;  // (a unit's first segment has no exit)
+    int64_t qa = 0;
+    int32_t qprev = 0, q0 = 0;
+    if (live) {
+      qa = units[sg.unit].a + sg.start;
+      qprev = segs[si - 1].qcount;
+      q0 = qn[qa];
+    }
+    for (uint64_t m = __ballot(live); m != 0; m &= m - 1) {
+      const int src = __builtin_ctzll(m);
+      const int32_t s0 = __builtin_amdgcn_readlane(sg.start, src);
+      const int32_t len = __builtin_amdgcn_readlane(sg.len, src);
+      const int32_t nq = __builtin_amdgcn_readlane(sg.qcount, src);
+      const int32_t qp = __builtin_amdgcn_readlane(qprev, src);
+      const int32_t q0u = __builtin_amdgcn_readlane(q0, src);
+      const int64_t at = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(qa >> 32), src) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int32_t)qa, src));
+      const int32_t* __restrict__ spar = par + (at - s0);  // indexed by row
+      const int32_t* __restrict__ sext = exta + (at - s0);
+      const int32_t s1 = s0 + len;
+      for (int32_t wb = 0; wb < nq; wb += 64) {  // (more than 64 max-level nodes: 64 walkers at a time)
+        const bool mine = wb + l < nq;
+        int32_t pos = -2;  // a walker's row; negative: -2 - (its exit), the walk is over
+        if (mine) {
+          pos = nq == 1 ? q0u : qn[at + wb + l];
+          if (pos < s0 || pos >= s1) {  // (cannot happen for the kernels' own output)
+            raise_error(err, kErrCorrupt);
+            pos = -2;
+          }
+        }
+        for (int32_t k = (len - 1) >> 6; k >= 0 && __ballot(pos >= 0) != 0; k -= 4) {
+          int32_t pv[4], ev[4];
+#pragma unroll
+          for (int g = 0; g < 4; g++) {
+            const int32_t r = s0 + 64 * (k - g) + l;
+            pv[g] = (k - g >= 0 && r < s1) ? spar[r] : -2;
+          }
+#pragma unroll
+          for (int g = 0; g < 4; g++) {  // anchors, where the outside parent's ordinal is past the list
+            const int32_t r = s0 + 64 * (k - g) + l;
+            ev[g] = (pv[g] < 0 && -2 - pv[g] >= qp) ? sext[r] : 0;
+          }
+#pragma unroll
+          for (int g = 0; g < 4; g++) {
+            if (k - g < 0) break;
+            const int32_t c0 = s0 + 64 * (k - g);
+            int32_t cur = pv[g];
+            if (cur < 0 && -2 - cur >= qp) cur = ev[g];
+            if (cur == -1 || (cur >= 0 && (cur < s0 || cur >= c0 + l))) {  // (cannot happen: steps lead down)
+              raise_error(err, kErrCorrupt);
+              cur = -2;
+            }
+            while (true) {
+              const bool inb = cur >= c0;
+              if (__ballot(inb) == 0) break;
+              const int32_t t = __builtin_amdgcn_ds_bpermute((cur - c0) << 2, cur);
+              cur = inb ? t : cur;
+            }
+            const int32_t t = __builtin_amdgcn_ds_bpermute((pos - c0) << 2, cur);
+            pos = pos >= c0 ? t : pos;
+            if (__ballot(pos >= 0) == 0) break;
+          }
+        }
+        if (pos >= 0) {  // (a walk that has not ended at the segment's first row: cannot happen)
+          raise_error(err, kErrCorrupt);
+          pos = -2;
+        }
+        if (mine) qexit[at + wb + l] = -2 - pos;
+      }
+    }
+  }
 }
 
 // Per unit: chain entry index of every segment, last to first; chain length.
