@@ -273,3 +273,57 @@ def test_chain_deep_levels_vs_oracle(reach):
         elif c.decode_stream(got) != O.decode(want):
             bad.append((t, n, "tables"))
     assert not bad, bad
+
+
+def _stitch_blocks(kind, rng):
+    """Blocks that are closed prefixes (segments) of one table's permutation, of a given shape."""
+    pool = [1, 2, 63, 64, 65, 130, 255, 256, 257, 700, 1500]
+    if kind in ("saw", "rise_then_fall"):  # (thousands of open lists at once run in the slowest chain tier)
+        pool.append(6000)
+    sizes = [int(x) for x in rng.choice(pool, size=int(rng.integers(4, 9)))]
+    out, base = [], 0
+    for L in sizes:
+        if kind == "falling":  # every row ends a list of its own
+            blk = list(range(L - 1, -1, -1))
+        elif kind == "rise_then_fall":  # a rising run, then many rows that all end at the top level
+            k = max(1, L // 3)
+            blk = list(range(k)) + list(range(L - 1, k - 1, -1))
+        elif kind == "fall_then_rise":
+            k = max(1, L // 2)
+            blk = list(range(L - 1, L - 1 - k, -1)) + list(range(L - k))
+        elif kind == "saw":  # short falling teeth on a rising line, under one long edge
+            blk = []
+            t = int(rng.integers(2, 9))
+            for a in range(0, L - 1, t):
+                blk += list(range(min(a + t, L - 1) - 1, a - 1, -1))
+            blk = [L - 1] + blk
+        else:  # random
+            blk = [int(x) for x in rng.permutation(L)]
+        assert sorted(blk) == list(range(L)), (kind, L)
+        out += [base + v for v in blk]
+        base += L
+    return out
+
+
+@pytest.mark.parametrize("kind", ["falling", "rise_then_fall", "fall_then_rise", "saw", "random"])
+def test_chain_stitching_shapes_vs_oracle(kind):
+    """Segments with many max-level rows (more than a wave has lanes), with many rows whose
+    outside parent comes from an anchor, and of lengths on either side of the 64-row chunks
+    and 256-row groups in which the exits are swept; the permutation and its inverse."""
+    rng = np.random.default_rng(len(kind) * 131 + 7)
+    c = ctx(131072)
+    bad = []
+    for t in range(5):
+        order = _stitch_blocks(kind, rng)
+        inv = [0] * len(order)
+        for i, v in enumerate(order):
+            inv[v] = i
+        for which, perm in (("perm", order), ("inverse", inv)):
+            recs = S.permutation_stream(perm, src=2)
+            want, _ = O.encode(recs, 131072)
+            got = c.encode_stream(recs)
+            if got != want:
+                bad.append((t, which, len(perm), first_diff(got, want)))
+            elif c.decode_stream(got) != O.decode(want):
+                bad.append((t, which, len(perm), "tables"))
+    assert not bad, bad
