@@ -144,6 +144,11 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
   auto ring_par = [&](int32_t x) -> int32_t {  // parent of row x < i of this segment
     int32_t p = ring[x & (R - 1)].x;
     asm volatile("" : "+v"(p));  // keeps the LDS read an LDS read (no flat load of a selected address)
+#ifdef CDCX_CHAIN_STATS
+    if (x < i - R) atomicAdd(&g8_stats[22], 1ull);
+    if (x < i - 32) atomicAdd(&g8_stats[23], 1ull);
+    if (x < i - 16) atomicAdd(&g8_stats[19], 1ull);
+#endif
     if (x < i - R) p = ldg(par, ab + 4u * (uint32_t)x);
     return p;
   };

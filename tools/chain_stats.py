@@ -11,7 +11,7 @@ from rempi_amd import cdcx  # noqa: E402
 
 NAMES = ["wave iterations", "fetch path", "body", "useB", "binsearch", "binsearch steps", "ks>=1", "need", "climb steps A",
          "interior ok", "root", "exta", "topg spill (grow)", "topg update", "qn store", "sweep path", "sweep compaction A",
-         "sweep compaction B", "overflow", "", "segments fetched", "active lanes in body"]
+         "sweep compaction B", "overflow", "ring reads > 16 rows back", "segments fetched", "active lanes in body", "ring reads > 64 rows back (global)", "ring reads > 32 rows back"]
 
 ranks = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 p = rempi_amd.default_gen_params(world_size=1024, events_per_rank=10_000_000)
