@@ -860,12 +860,13 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
             d_idd, d_dld, d_perm, d_cinv, d_nfail);
   // The record tiles are listed while the rebuild runs; the reconstruction itself is launched
   // before the wait for the failure count when no unit can have failed into a later tier.
-  int2* d_rt = nullptr;
+  int4* d_rt = nullptr;
   int32_t* d_recs = nullptr;
   if (records) {
-    d_rt = c->buf<int2>("d_rec_tiles", tot.rec_tiles);
+    d_rt = c->buf<int4>("d_rec_tiles", tot.rec_tiles);
     d_recs = c->buf<int32_t>(kAliasRecs, 8 * ro);
-    c->launch(K_LISTS, k_dec_fill_tiles, dim3(NU), dim3(256), s, (const DUnit*)d_units, (const int32_t*)d_rt0, d_rt);
+    c->launch(K_LISTS, k_dec_fill_tiles, dim3(NU), dim3(256), s, (const DUnit*)d_units, (const int32_t*)d_rt0,
+              (const uint64_t*)d_uidd, d_rt);
   }
   // An input the kernels flagged must not reach the record reconstruction (it trusts the
   // sections' checks and the permutation): the error word travels with the failure count.
@@ -896,7 +897,7 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   c->n_rec_out = ro;
   if (records) {
     c->launch(K_DEC_RECORDS, k_dec_records, dim3((unsigned)tot.rec_tiles), dim3(256), s, (const DUnit*)d_units,
-              (const int2*)d_rt, d_in, (const int32_t*)d_cinv, (const uint8_t*)d_wnf, (const uint64_t*)d_uidd, d_keys,
+              (const int4*)d_rt, d_in, (const int32_t*)d_cinv, (const uint8_t*)d_wnf, (const uint64_t*)d_uidd, d_keys,
               (int4*)d_recs);
     c->d_rec_out = d_recs;
   }

@@ -89,7 +89,7 @@ __global__ void k_out_layout(Unit*, Chunk*, int32_t, const int32_t*, int32_t, co
 __global__ void k_dec_scan_chunks(const int32_t*, int32_t, int32_t*, DecTotals*);
 __global__ void k_dec_scan_units(DUnit*, int32_t, int32_t, int32_t*, DecTotals*);
 __global__ void k_dec_order(const DUnit*, int32_t, int32_t*);
-__global__ void k_dec_fill_tiles(const DUnit*, const int32_t*, int2*);
+__global__ void k_dec_fill_tiles(const DUnit*, const int32_t*, const uint64_t*, int4*);
 
 // decode.hip
 __global__ void k_dec_count_chunks(const uint8_t*, const int64_t*, const int64_t*, int32_t, int32_t*, uint32_t*);
@@ -104,7 +104,7 @@ __global__ void k_dec_perm_grp(DUnit*, const int32_t*, int32_t, const uint8_t*, 
 __global__ void k_dec_cinv(const DUnit*, const int32_t*, int32_t*);
 template <int K>
 __global__ void k_dec_perm_window(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
-__global__ void k_dec_records(const DUnit*, const int2*, const uint8_t*, const int32_t*, const uint8_t*, const uint64_t*,
+__global__ void k_dec_records(const DUnit*, const int4*, const uint8_t*, const int32_t*, const uint8_t*, const uint64_t*,
                               const int2*, int4*);
 __global__ void k_verify_roundtrip(const Unit*, const int64_t*, const int64_t*, const TRec*, const int4*, const int4*,
                                    unsigned long long*);

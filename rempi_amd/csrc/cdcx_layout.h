@@ -16,6 +16,7 @@ namespace cdcx {
 constexpr int kMaxSets = 256;       // matching_set_id in [0, 256)
 constexpr int kTile = 1024;         // records per tile in record-parallel kernels
 constexpr int kSortTile = 1024;     // matched events per LDS sort tile
+constexpr int kRecTile = 1024;      // decoded rows per tile of the record reconstruction
 constexpr int kRankWin = 64;        // k_window_rank: D (pairs more than D apart must be in order)
 constexpr int kMaxUnitSources = 2048;  // distinct sources per unit held in LDS (epoch)
 

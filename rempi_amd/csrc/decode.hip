@@ -686,34 +686,22 @@ __global__ void __launch_bounds__(256) k_dec_cinv(const DUnit* __restrict__ unit
 // matched_index; unmatched run k with id `id` sits right before matched row `id`, so row
 // i lands at i + #runs with id <= i.  The run ids were checked strictly increasing by
 // k_dec_sections, so a tile finds its runs by binary search and ranks rows with one scan.
-__global__ void __launch_bounds__(256) k_dec_records(const DUnit* __restrict__ units, const int2* __restrict__ tiles,
+__global__ void __launch_bounds__(256) k_dec_records(const DUnit* __restrict__ units, const int4* __restrict__ tiles,
                                                      const uint8_t* __restrict__ in, const int32_t* __restrict__ cinv,
                                                      const uint8_t* __restrict__ wnf, const uint64_t* __restrict__ uidd,
                                                      const int2* __restrict__ keys, int4* __restrict__ rec) {
-  constexpr int TR = 1024, PER = TR / 256;
+  constexpr int TR = kRecTile, PER = TR / 256;
   __shared__ int32_t mk[TR + 1];
-  __shared__ int32_t rlo, rhi;
   __shared__ int32_t lds[4];
-  const int2 T = tiles[blockIdx.x];
+  const int4 T = tiles[blockIdx.x];  // {unit, tile, first and past-the-last run of the tile} (k_dec_fill_tiles)
   const DUnit u = units[T.x];
   const int32_t M = u.M;
-  const int32_t U = (u.Uc > 0) ? u.U : 0;
   const int32_t i0 = T.y * TR;
   const int32_t n = max(0, min(TR, M - i0));
-  const bool last = i0 + TR >= M;
   const uint64_t* ids = uidd + u.wbase;
   for (int r = threadIdx.x; r <= TR; r += 256) mk[r] = 0;
-  if (threadIdx.x < 2) {
-    const uint64_t key = (threadIdx.x == 0) ? (uint64_t)i0 : (last ? (uint64_t)M + 1 : (uint64_t)(i0 + TR));
-    int32_t lo = 0, hi = U;
-    while (lo < hi) {
-      const int32_t mid = (lo + hi) >> 1;
-      if (ids[mid] < key) lo = mid + 1; else hi = mid;
-    }
-    if (threadIdx.x == 0) rlo = lo; else rhi = lo;
-  }
   __syncthreads();
-  const int32_t lo = rlo, hi = rhi;
+  const int32_t lo = T.z, hi = T.w;
   for (int32_t k = lo + threadIdx.x; k < hi; k += 256) {
     const int32_t id = (int32_t)ids[k];
     mk[id - i0] = 1;

@@ -24,24 +24,48 @@ namespace cdcx {
 __global__ void __launch_bounds__(256) k_tile_hist(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
                                                    uint32_t* __restrict__ hist, uint32_t* __restrict__ presence,
                                                    uint32_t* err) {
-  __shared__ uint32_t h[kMaxSets];
-  __shared__ uint32_t last[kMaxSets];  // max over the set's records of (index in tile + 1) << 1 | matched
-  h[threadIdx.x] = 0;
-  last[threadIdx.x] = 0;
+  // A rank has a handful of sets, so the 64 lanes of an LDS atomic mostly meet on one address
+  // and are served one after the other.  Eight copies of the two tables, picked by lane % 8 and
+  // one bank apart, cut that to eight lanes per address; the copies are merged at the end.
+  constexpr int kCopies = 8, kStride = kMaxSets + 1;
+  __shared__ uint32_t h[kCopies * kStride];
+  __shared__ uint32_t last[kCopies * kStride];  // max over the set's records of (index in tile + 1) << 1 | matched
+  for (int q = threadIdx.x; q < kCopies * kStride; q += 256) {
+    h[q] = 0;
+    last[q] = 0;
+  }
   __syncthreads();
   const Tile t = tiles[blockIdx.x];
-  for (int i = threadIdx.x; i < t.len; i += blockDim.x) {
-    const int32_t* rp = rec + (t.start + i) * 8;
-    const int32_t sid = rp[7];
+  const int cp = (threadIdx.x & (kCopies - 1)) * kStride;
+  // (all of the tile's loads are issued before the first atomic: one memory round trip per block)
+  constexpr int PER = kTile / 256;
+  int32_t sidv[PER], flv[PER];
+#pragma unroll
+  for (int q = 0; q < PER; q++) {
+    const int i = q * 256 + threadIdx.x;
+    const int32_t* rp = rec + (t.start + min(i, t.len - 1)) * 8;  // (rows past the tile's end re-read its last record)
+    sidv[q] = t.len > 0 ? rp[7] : 0;
+    flv[q] = t.len > 0 ? rp[2] : 0;
+  }
+#pragma unroll
+  for (int q = 0; q < PER; q++) {
+    const int i = q * 256 + threadIdx.x;
+    if (i >= t.len) break;
+    const int32_t sid = sidv[q];
     if ((uint32_t)sid >= (uint32_t)kMaxSets) raise_error(err, kErrLimit);
     else {
-      atomicAdd(&h[sid], 1u);
-      atomicMax(&last[sid], ((uint32_t)(i + 1) << 1) | (rp[2] == 1 ? 1u : 0u));
+      atomicAdd(&h[cp + sid], 1u);
+      atomicMax(&last[cp + sid], ((uint32_t)(i + 1) << 1) | (flv[q] == 1 ? 1u : 0u));
     }
   }
   __syncthreads();
-  const uint32_t v = h[threadIdx.x];
-  hist[(int64_t)blockIdx.x * kMaxSets + threadIdx.x] = v | ((last[threadIdx.x] & 1u) << 31);
+  uint32_t v = 0, lm = 0;
+#pragma unroll
+  for (int q = 0; q < kCopies; q++) {
+    v += h[q * kStride + threadIdx.x];
+    lm = max(lm, last[q * kStride + threadIdx.x]);
+  }
+  hist[(int64_t)blockIdx.x * kMaxSets + threadIdx.x] = v | ((lm & 1u) << 31);
   const uint64_t nz = __builtin_amdgcn_ballot_w64(v != 0);
   if (lane_id() == 0 && (uint32_t)nz) atomicOr(&presence[t.rank * (kMaxSets / 32) + wave_id() * 2], (uint32_t)nz);
   if (lane_id() == 32 && (uint32_t)(nz >> 32)) atomicOr(&presence[t.rank * (kMaxSets / 32) + wave_id() * 2 + 1], (uint32_t)(nz >> 32));

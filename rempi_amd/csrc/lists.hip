@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(kScanBlock) k_dec_scan_units(DUnit* __restrict
     const int64_t w0 = scan_round(ok ? M + 1 : 0, cw, lds);
     const int64_t r0 = scan_round(M + nrun, cr, lds);
     const int64_t k0 = scan_round(M, ck, lds);
-    const int64_t t0 = scan_round((int64_t)((ok && (M > 0 || nrun > 0)) ? max((M + 1023) / 1024, (int64_t)1) : 0), ct, lds);
+    const int64_t t0 = scan_round((int64_t)((ok && (M > 0 || nrun > 0)) ? max((M + kRecTile - 1) / kRecTile, (int64_t)1) : 0), ct, lds);
     if (ok) {
       units[q].wbase = w0;
       units[q].rec_off = r0;
@@ -333,11 +333,27 @@ __global__ void __launch_bounds__(256) k_dec_order(const DUnit* __restrict__ uni
 // Record tiles of k_dec_records: {unit, tile} for every 1024 matched rows of a unit (at least
 // one tile for a unit that only holds unmatched runs).
 __global__ void __launch_bounds__(256) k_dec_fill_tiles(const DUnit* __restrict__ units, const int32_t* __restrict__ tile0,
-                                                        int2* __restrict__ tiles) {
+                                                        const uint64_t* __restrict__ uidd, int4* __restrict__ tiles) {
   latency_kernel();
   const int32_t q = blockIdx.x;
+  const DUnit u = units[q];
   const int32_t t0 = tile0[q], n = tile0[q + 1] - t0;
-  for (int32_t k = threadIdx.x; k < n; k += 256) tiles[t0 + k] = make_int2(q, k);
+  const int32_t U = (u.Uc > 0) ? u.U : 0;
+  const uint64_t* ids = uidd + u.wbase;
+  // the unmatched runs that precede the tile's rows (ids ascending; a run with id == M follows the last row)
+  auto lower = [&](uint64_t key) {
+    int32_t lo = 0, hi = U;
+    while (lo < hi) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (ids[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+  };
+  for (int32_t k = threadIdx.x; k < n; k += 256) {
+    const int64_t i0 = (int64_t)k * kRecTile;
+    const bool last = i0 + kRecTile >= u.M;
+    tiles[t0 + k] = make_int4(q, k, lower((uint64_t)i0), lower(last ? (uint64_t)u.M + 1 : (uint64_t)(i0 + kRecTile)));
+  }
 }
 
 }  // namespace cdcx
