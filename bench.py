@@ -50,7 +50,7 @@ FIXTURE = os.path.join(ROOT, "tests", "golden", "config3_full.json")
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--world", type=int, default=1024, help="ranks in the traced job")
     ap.add_argument("--events", type=int, default=10_000_000, help="events per rank trace")
