@@ -136,7 +136,10 @@ struct Gate {
   hipEvent_t last[4] = {nullptr, nullptr, nullptr, nullptr};
   const void* owner[4] = {nullptr, nullptr, nullptr, nullptr};
 };
-constexpr int kGateKinds = 2;    // 0: chain, 1: permutation rebuild
+// 0: chain, 1: permutation rebuild, 2: the scatter (CDCX_GATE bit 3) -- bandwidth-bound; two of
+// them side by side share the HBM and both take twice as long, one at a time gives each lane
+// its T-order records sooner
+constexpr int kGateKinds = 3;
 constexpr int kGateDevices = 16;
 static Gate g_gates[kGateDevices][kGateKinds];
 
@@ -205,12 +208,16 @@ struct cdcx_ctx {
   bool chain_g16 = getenv("CDCX_CHAIN_G16") != nullptr;  // first tier on 16-lane groups (A/B timing)
   // segments of at least this many events run at raised wave priority in the 8-lane chain tier
   int chain_long = getenv("CDCX_CHAIN_LONG") ? atoi(getenv("CDCX_CHAIN_LONG")) : 1536;
-  // gates in use: bit 0 chain, bit 1 permutation rebuild, bit 2 both kinds through one gate
+  // which bandwidth-bound kernels take turns on gate 2 (bits: tile_hist, scatter, unit_prep, dec_records,
+  // positions, write_units, deltas, window_rank)
+  int gate_bw = getenv("CDCX_GATE_BW") ? atoi(getenv("CDCX_GATE_BW")) : 2;
+  // gates in use: bit 0 chain, bit 1 permutation rebuild, bit 2 both kinds through one gate, bit 3 scatter
   // (on the bench batch: + 1 % over 3 steps from a common start, + 2.7 % over 12 steps)
-  int gate_mode = getenv("CDCX_GATE") ? atoi(getenv("CDCX_GATE")) : 3;
+  int gate_mode = getenv("CDCX_GATE") ? atoi(getenv("CDCX_GATE")) : 11;
   // kernels of a kind allowed side by side (1 .. 4): {chain, permutation rebuild}
   int gate_depth[kGateKinds] = {getenv("CDCX_GATE_CHAIN") ? atoi(getenv("CDCX_GATE_CHAIN")) : 1,
-                                getenv("CDCX_GATE_PERM") ? atoi(getenv("CDCX_GATE_PERM")) : 2};
+                                getenv("CDCX_GATE_PERM") ? atoi(getenv("CDCX_GATE_PERM")) : 2,
+                                getenv("CDCX_GATE_SCATTER") ? atoi(getenv("CDCX_GATE_SCATTER")) : 1};
   hipEvent_t gate_ev[kGateKinds][4] = {};
   int gate_next[kGateKinds] = {};
   int64_t chain_tier_counts[3] = {0, 0, 0};  // segments entering each tier in the last encode
@@ -287,7 +294,7 @@ struct cdcx_ctx {
   // hundred tables is bound by latency, not by issue) would only wait.
   template <class K, class... Args>
   void launch_gated(int kind, bool big, int kid, K kernel, dim3 g, dim3 b, hipStream_t s, Args... args) {
-    if (!big || !((gate_mode >> kind) & 1) || device >= kGateDevices) {
+    if (!big || !((gate_mode >> (kind == 2 ? 3 : kind)) & 1) || device >= kGateDevices) {
       launch(kid, kernel, g, b, s, args...);
       return;
     }
@@ -470,12 +477,12 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int2* d_chunk_cap = c->buf<int2>("chunk_cap", ccap_off[R]);
   int32_t* d_nchunks = c->buf<int32_t>("nchunks", R);
 
-  c->launch(K_TILE_HIST, k_tile_hist, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, d_hist, d_presence, d_err);
+  c->launch_gated(2, NT >= 65536 && (c->gate_bw & 1), K_TILE_HIST, k_tile_hist, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, d_hist, d_presence, d_err);
   c->launch(K_SET_DENSE, k_set_dense, dim3(R), dim3(kMaxSets), s, (const uint32_t*)d_presence, d_dense, d_setlist, d_nsets);
   c->launch(K_HIST_SCAN, k_hist_scan, dim3(R), dim3(256), s, (const uint32_t*)d_hist, (const int32_t*)d_tile0,
             (const int32_t*)d_ntiles, (const int32_t*)d_nsets, (const int32_t*)d_setlist, d_base, d_tstart, d_prevm);
   // (the scatter also forms the records' length increments and their tile sums)
-  c->launch(K_SCATTER, k_scatter, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, (const int16_t*)d_dense,
+  c->launch_gated(2, NT >= 65536 && (c->gate_bw & 2), K_SCATTER, k_scatter, dim3(NT), dim3(256), s, d_rec, (const Tile*)d_tiles, (const int16_t*)d_dense,
             (const int32_t*)d_base, (const uint8_t*)d_prevm, (const int32_t*)d_nsets, (const int64_t*)d_rec_off, d_trec,
             d_inc0, d_tsum);
   c->launch(K_RANK_SCAN, k_rank_scan, dim3(R), dim3(256), s, (const int32_t*)d_tsum, (const int32_t*)d_tile0,
@@ -537,7 +544,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int32_t* d_wp = c->buf<int32_t>("wp", N);
   int32_t* d_run_id = c->buf<int32_t>("run_id", N);
   uint64_t* d_run_cnt = c->buf<uint64_t>("run_cnt", N);
-  c->launch(K_UNIT_PREP, k_unit_prep, dim3((unsigned)lbn), dim3(256), s, d_units, (const TRec*)d_trec, d_mkey, d_midx, d_wp,
+  c->launch_gated(2, NT >= 65536 && (c->gate_bw & 4), K_UNIT_PREP, k_unit_prep, dim3((unsigned)lbn), dim3(256), s, d_units, (const TRec*)d_trec, d_mkey, d_midx, d_wp,
             d_run_id, d_run_cnt, d_err);
 
   // Clock-order rank: the windowed pass for every unit (tiles of kSortTile events); the units
@@ -553,7 +560,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   uint64_t* d_skey = c->buf<uint64_t>("skey", N);
   if (c->rank_tier == 0)
   {
-    c->launch(K_WINDOW_RANK, k_window_rank, dim3((unsigned)NSmax), dim3(256), s, d_units, (const SortTile*)d_st,
+    c->launch_gated(2, NT >= 65536 && (c->gate_bw & 128), K_WINDOW_RANK, k_window_rank, dim3((unsigned)NSmax), dim3(256), s, d_units, (const SortTile*)d_st,
               (const uint64_t*)d_mkey, d_cord, d_inv, d_skey);
     c->launch(K_WINDOW_RANK, k_window_rank_wide, dim3((unsigned)lbn), dim3(256), s, d_units, (const uint64_t*)d_mkey, d_cord,
               d_inv, d_skey);
@@ -731,16 +738,16 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int32_t* d_crow = c->buf<int32_t>("crow", N);
   uint32_t* d_seq = c->buf<uint32_t>("seq", 2 * N);
   int32_t* d_sx = c->buf<int32_t>("sx", 2 * N);
-  c->launch(K_POSITIONS, k_pos_rows, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_cord,
+  c->launch_gated(2, NU >= 4096 && (c->gate_bw & 16), K_POSITIONS, k_pos_rows, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_cord,
             (const uint8_t*)d_chain, d_posA, d_crow);
-  c->launch(K_POSITIONS, k_pos_cols, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_inv,
+  c->launch_gated(2, NU >= 4096 && (c->gate_bw & 16), K_POSITIONS, k_pos_cols, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_inv,
             (const uint8_t*)d_chain, (const int32_t*)d_posA, (const int32_t*)d_crow, d_seq, d_sx);
-  c->launch(K_DELTAS, k_deltas, dim3(NU), dim3(256), s, (const Unit*)d_units, (const uint32_t*)d_seq, (const int32_t*)d_sx,
+  c->launch_gated(2, NU >= 4096 && (c->gate_bw & 64), K_DELTAS, k_deltas, dim3(NU), dim3(256), s, (const Unit*)d_units, (const uint32_t*)d_seq, (const int32_t*)d_sx,
             d_out);
   }
 
   if (c->rep) out_layout();
-  c->launch(K_WRITE_UNITS, k_write_units, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_midx,
+  c->launch_gated(2, NU >= 4096 && (c->gate_bw & 32), K_WRITE_UNITS, k_write_units, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_midx,
             (const int32_t*)d_wp, (const int32_t*)d_run_id, (const uint64_t*)d_run_cnt, (const uint64_t*)d_ep_rank,
             (const uint64_t*)d_ep_clk, (int32_t)c->rep, d_out);
   c->launch(K_CHUNK_HEADERS, k_chunk_headers, dim3(blocks(C, 256)), dim3(256), s, (const Chunk*)d_chunks, C, d_out);
@@ -896,7 +903,7 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   c->d_perm = d_perm;
   c->n_rec_out = ro;
   if (records) {
-    c->launch(K_DEC_RECORDS, k_dec_records, dim3((unsigned)tot.rec_tiles), dim3(256), s, (const DUnit*)d_units,
+    c->launch_gated(2, NU >= 4096 && (c->gate_bw & 8), K_DEC_RECORDS, k_dec_records, dim3((unsigned)tot.rec_tiles), dim3(256), s, (const DUnit*)d_units,
               (const int4*)d_rt, d_in, (const int32_t*)d_cinv, (const uint8_t*)d_wnf, (const uint64_t*)d_uidd, d_keys,
               (int4*)d_recs);
     c->d_rec_out = d_recs;
