@@ -216,7 +216,7 @@ struct cdcx_ctx {
   int gate_mode = getenv("CDCX_GATE") ? atoi(getenv("CDCX_GATE")) : 11;
   // kernels of a kind allowed side by side (1 .. 4): {chain, permutation rebuild}
   int gate_depth[kGateKinds] = {getenv("CDCX_GATE_CHAIN") ? atoi(getenv("CDCX_GATE_CHAIN")) : 1,
-                                getenv("CDCX_GATE_PERM") ? atoi(getenv("CDCX_GATE_PERM")) : 2,
+                                getenv("CDCX_GATE_PERM") ? atoi(getenv("CDCX_GATE_PERM")) : 1,
                                 getenv("CDCX_GATE_SCATTER") ? atoi(getenv("CDCX_GATE_SCATTER")) : 1};
   hipEvent_t gate_ev[kGateKinds][4] = {};
   int gate_next[kGateKinds] = {};
