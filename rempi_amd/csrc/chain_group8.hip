@@ -42,7 +42,7 @@ namespace cdcx {
 
 namespace {
 constexpr int G8 = 8;
-constexpr int kRing8 = 64;      // rows of {par, column} per group in LDS
+constexpr int kRing8 = 32;      // rows of {par, column} per group in LDS
 constexpr int kTopRing = 32;    // spilled tops per group in LDS: one 128-byte line of topg
 constexpr int kQBuf = 8;        // max-level rows per group kept in LDS until the segment ends
 
