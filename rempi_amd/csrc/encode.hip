@@ -25,9 +25,11 @@ __global__ void __launch_bounds__(256) k_tile_hist(const int32_t* __restrict__ r
                                                    uint32_t* __restrict__ hist, uint32_t* __restrict__ presence,
                                                    uint32_t* err) {
   // A rank has a handful of sets, so the 64 lanes of an LDS atomic mostly meet on one address
-  // and are served one after the other.  Eight copies of the two tables, picked by lane % 8 and
-  // one bank apart, cut that to eight lanes per address; the copies are merged at the end.
-  constexpr int kCopies = 8, kStride = kMaxSets + 1;
+  // and are served one after the other.  Four copies of the two tables, picked by lane % 4 and
+  // one bank apart, cut that to sixteen lanes per address; the copies are merged at the end.
+  // (Eight copies are faster alone and slower beside the other lanes' kernels: LDS is what the
+  // kernels of a busy GPU run short of first.)
+  constexpr int kCopies = 4, kStride = kMaxSets + 1;
   __shared__ uint32_t h[kCopies * kStride];
   __shared__ uint32_t last[kCopies * kStride];  // max over the set's records of (index in tile + 1) << 1 | matched
   for (int q = threadIdx.x; q < kCopies * kStride; q += 256) {
@@ -141,10 +143,13 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
                                                  const int64_t* __restrict__ rec_off, TRec* __restrict__ trec,
                                                  uint8_t* __restrict__ inc0s, int32_t* __restrict__ tsum) {
   constexpr int ROUNDS = kTile / 256;
-  __shared__ int32_t wc[ROUNDS * 4 * kMaxSets];  // [round][wave][table]: count | last record's flags << 16
+  // [round][wave][table]: count (then the count before the slot) | last record's flags << 12; half words,
+  // since LDS is what the kernels of a busy GPU run short of first
+  __shared__ uint16_t wc[ROUNDS * 4 * kMaxSets];
+  static_assert(kTile < (1 << 12), "a tile's count must fit the low 12 bits");
   __shared__ int32_t lds[4];
   __shared__ uint8_t incs[kTile];  // the tile's flags, gathered so that a thread stores four consecutive ones
-  for (int i = threadIdx.x; i < ROUNDS * 4 * kMaxSets; i += 256) wc[i] = 0;
+  for (int i = threadIdx.x; i < ROUNDS * 4 * kMaxSets / 2; i += 256) reinterpret_cast<uint32_t*>(wc)[i] = 0;
   const Tile t = tiles[blockIdx.x];
   const int w = wave_id(), l = lane_id();
   const uint64_t lt_mask = (l == 0) ? 0ull : (~0ull >> (64 - l));
@@ -185,7 +190,7 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
     my_prev[j] = lower ? (1 | (int)(((mm >> (63 - __clzll((long long)lower))) & 1) << 1)) : 0;
     if (valid && lower == 0)
       wc[(j * 4 + w) * kMaxSets + tb] =
-          __popcll(peers) | ((1 | (int)(((mm >> (63 - __clzll((long long)peers))) & 1) << 1)) << 16);
+          (uint16_t)(__popcll(peers) | ((1 | (int)(((mm >> (63 - __clzll((long long)peers))) & 1) << 1)) << 12));
   }
   __syncthreads();
   if ((int)threadIdx.x < T) {  // exclusive scan over (round, wave) for each table: thread = table
@@ -194,9 +199,9 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
     int32_t pf = prevm[(int64_t)blockIdx.x * kMaxSets + tb];
     for (int k = 0; k < ROUNDS * 4; k++) {
       const int32_t v = wc[k * kMaxSets + tb];
-      wc[k * kMaxSets + tb] = run | (pf << 16);
-      run += v & 0xffff;
-      if (v >> 16) pf = v >> 16;
+      wc[k * kMaxSets + tb] = (uint16_t)(run | (pf << 12));
+      run += v & 0xfff;
+      if (v >> 12) pf = v >> 12;
     }
   }
   __syncthreads();
@@ -212,7 +217,7 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
     if (i >= t.len) continue;
     const int tb = my_t[j];
     const int32_t slot = wc[(j * 4 + w) * kMaxSets + tb];
-    const uint32_t pos = (uint32_t)(base_b[(uint32_t)tb] + (slot & 0xffff) + my_rank[j]);
+    const uint32_t pos = (uint32_t)(base_b[(uint32_t)tb] + (slot & 0xfff) + my_rank[j]);
     // lo = {count, type, flag, rank}, hi = {with_next, index, clock, set}
     TRec o;
     const bool matched = (lo[j].z == 1);
@@ -221,7 +226,7 @@ __global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec
     o.x = matched ? hi[j].y : lo[j].x;
     o.info = (matched ? (kInfoMatched | (hi[j].x != 0 ? kInfoWithNext : 0u)) : 0u) | (uint32_t)(spos0 + i);
     trec_r[pos] = o;
-    const int prev = my_prev[j] ? my_prev[j] : (slot >> 16);
+    const int prev = my_prev[j] ? my_prev[j] : (slot >> 12);
     const int32_t inc = (matched || prev != 1) ? 1 : 0;
     incs[i] = (uint8_t)inc;
     sum += inc;
