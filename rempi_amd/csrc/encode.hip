@@ -1370,17 +1370,26 @@ __global__ void __launch_bounds__(256) k_footer_order(const Unit* __restrict__ u
     }
     return;
   }
-  // Compact into the upper half of the hash arrays' storage, then bitonic sort by order.
-  __shared__ int32_t lkey[LCAP];
-  __shared__ unsigned long long lord[LCAP];
+  // Compact the table into the front of its own storage (every thread first takes its share of
+  // the slots into registers), then bitonic sort by order.
+  int32_t* const lkey = hkey;
+  unsigned long long* const lord = hord;
   __shared__ int32_t cnt;
+  int32_t ck[HC / 256];
+  unsigned long long co[HC / 256];
+#pragma unroll
+  for (int q = 0; q < HC / 256; q++) {
+    ck[q] = hkey[q * 256 + threadIdx.x];
+    co[q] = hord[q * 256 + threadIdx.x];
+  }
   if (threadIdx.x == 0) cnt = 0;
   __syncthreads();
-  for (int i = threadIdx.x; i < HC; i += 256) {
-    if (hkey[i] != INT32_MIN) {
-      const int q = atomicAdd(&cnt, 1);
-      lkey[q] = hkey[i];
-      lord[q] = hord[i];
+#pragma unroll
+  for (int q = 0; q < HC / 256; q++) {
+    if (ck[q] != INT32_MIN) {
+      const int at = atomicAdd(&cnt, 1);
+      lkey[at] = ck[q];
+      lord[at] = co[q];
     }
   }
   int P2 = 1;
