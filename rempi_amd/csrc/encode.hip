@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(256) k_hist_scan(const uint32_t* __restrict__ 
 // tile (prevm).  inc0s is laid out per tile (tile * kTile + index), so a rank's flags are
 // contiguous from a kTile-aligned start; tsum = the tile's sum.  A record's stream position
 // travels in its T-order record (TRec::info), which the chunk and unit searches read.
-__global__ void __launch_bounds__(256) k_scatter(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
+__global__ void __launch_bounds__(256, 8) k_scatter(const int32_t* __restrict__ rec, const Tile* __restrict__ tiles,
                                                  const int16_t* __restrict__ dense, const int32_t* __restrict__ base,
                                                  const uint8_t* __restrict__ prevm, const int32_t* __restrict__ nsets,
                                                  const int64_t* __restrict__ rec_off, TRec* __restrict__ trec,
