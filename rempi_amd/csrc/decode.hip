@@ -475,7 +475,6 @@ namespace {
 constexpr int32_t kGW = 128;     // window slots per group (power of two)
 constexpr int32_t kGMap = 256;   // element map entries per group (power of two)
 constexpr int32_t kGAhead = 56;  // an untouched x is brought to >= kGAhead slots before the end
-constexpr int32_t kGMapMaxM = 0xffff00;  // units with more matched events go to the next tier (16-bit element tags)
 
 template <int N, int I = 0, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -508,14 +507,10 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
                                                      int32_t* __restrict__ nfail) {
   constexpr int32_t W = kGW, WM = kGW - 1, MM = kGMap - 1;
   __shared__ int32_t win_all[4][W + 16];      // + one dummy slot per lane
-  // element -> position, one word per element of the window at [element % kGMap]: bits 8..23 of
-  // the element above the low 16 bits of its absolute position (a slot is rewritten at least
-  // every kGMap positions, so 16 bits tell positions apart); + dummies
-  __shared__ uint32_t emap_all[4][kGMap + 16];
+  __shared__ int2 emap_all[4][kGMap + 16];    // {element, absolute position}; + dummies
   const int g = threadIdx.x >> 4, j = threadIdx.x & 15;
   int32_t* win = win_all[g];
-  uint32_t* emap = emap_all[g];
-  auto emap_word = [](int32_t v, int32_t at) { return ((uint32_t)v >> 8 << 16) | ((uint32_t)at & 0xffffu); };
+  int2* emap = emap_all[g];
   const int32_t oi = blockIdx.x * 4 + g;
   const int32_t ui = (oi < n_units) ? order[oi] : -1;
   int32_t M = 0, P = 0;
@@ -538,9 +533,9 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
   const int32_t* ydl = yid + P;
   int64_t czi = 0, cxi = 0, czd = 0, cxd = 0;  // inverse-LP carries (rempi_compression_util.cpp:157-168)
   for (int32_t q = j; q < W; q += 16) win[q] = q;
-  for (int32_t q = j; q < kGMap; q += 16) emap[q] = (q < W) ? emap_word(q, q) : ~0u;  // (no element below kGMapMaxM has that tag)
+  for (int32_t q = j; q < kGMap; q += 16) emap[q] = (q < W) ? make_int2(q, q) : make_int2(-1, -1);
   int32_t base = 0;
-  int32_t failv = (sim && M <= kGMapMaxM) ? 0 : 1;  // (a unit too long for the map's tags fails into the next tier)
+  int32_t failv = sim ? 0 : 1;
   const int32_t Pmax = __builtin_amdgcn_readfirstlane(wave_reduce(P, OpMax()));
   auto slide = [&](bool go) {  // settle [base, base+16), open [base+W, base+W+16) as identity
     const int32_t ph = go ? ((base + j) & WM) : W + j;
@@ -552,7 +547,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
     const int32_t e = base + W + j;
     __builtin_amdgcn_wave_barrier();
     win[ph] = e;
-    emap[go ? (e & MM) : kGMap + j] = emap_word(e, e);
+    emap[go ? (e & MM) : kGMap + j] = make_int2(e, e);
     if (go) base += 16;
   };
   // one pair of all four groups: x, d group-uniform
@@ -567,10 +562,10 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
       const bool far = act & (x >= base + W);
       if (__builtin_amdgcn_ballot_w64(far))
         while (__builtin_amdgcn_ballot_w64(far && x >= base + W - kGAhead)) slide(far && x >= base + W - kGAhead);
-      const uint32_t e = emap[act ? (x & MM) : kGMap + j];
-      int32_t p = (int32_t)((e - (uint32_t)base) & 0xffffu);
+      const int2 e = emap[act ? (x & MM) : kGMap + j];
+      int32_t p = e.y - base;
       int32_t t = p + d;
-      const bool bad = act & (((e >> 16) != ((uint32_t)x >> 8)) | ((uint32_t)p >= (uint32_t)W) | (t < 0) | (base + t > M - 1));
+      const bool bad = act & ((e.x != x) | ((uint32_t)p >= (uint32_t)W) | (t < 0) | (base + t > M - 1));
       failv |= bad ? 1 : 0;
       act &= !bad;
       if (__builtin_amdgcn_ballot_w64(act && t > W - 1)) {
@@ -599,7 +594,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
         const int32_t v = (o < len) ? w : x;
         __builtin_amdgcn_wave_barrier();
         win[sel ? ((base + s) & WM) : W + j] = v;
-        emap[sel ? (v & MM) : kGMap + j] = emap_word(v, base + s);
+        emap[sel ? (v & MM) : kGMap + j] = make_int2(v, base + s);
         __builtin_amdgcn_wave_barrier();
       };
       chunk(0);
