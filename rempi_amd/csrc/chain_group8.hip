@@ -110,9 +110,11 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
   constexpr int R = kRing8;
   __shared__ int32_t next_j;
   __shared__ int2 ring_all[kGroups][R];          // {par, column} of row r at [r % R]
+  __shared__ int32_t comp_all[kGroups][3 * 16];  // sweep compaction of a list that uses the B slots
   __shared__ int32_t tring_all[kGroups][kTopRing];  // spilled top of level e + 1 at [(tq + e) % 32]
   __shared__ int32_t qbuf_all[kGroups][kQBuf];
   int2* ring = ring_all[threadIdx.x / G];
+  int32_t* comp = comp_all[threadIdx.x / G];
   int32_t* tring = tring_all[threadIdx.x / G];
   int32_t* qbuf = qbuf_all[threadIdx.x / G];
   if (threadIdx.x == 0) next_j = 0;
@@ -394,28 +396,28 @@ __global__ void __launch_bounds__(256) k_chain_grp8(const Unit* __restrict__ uni
           dead |= grp8(sw & m_lt(j + G, nl) & m_lt(lcolB, c), sh) << G;
           if (m_ne((int32_t)dead, 0) != 0) {
             G8_STAT(17);
-            // compaction by ds_permute: slot s (alive) lands at s - #dead below it.  The new A
-            // slots take what the A slots send them and, past those, what the B slots send down;
-            // the new B slots what stays up.  A lane that has nothing to send aims at a slot
-            // whose result is not used: the last one, or slot 0 when the list still fills the A
-            // slots (slot 0 then comes from an A slot).
-            const uint32_t live = ~dead & ((1u << nl) - 1u);
-            const int32_t nA = __popc(live & 0xFFu), nn = __popc(live);
-            const bool aliveA = (live >> j) & 1u, aliveB = (live >> (j + G)) & 1u;
-            const int32_t dB = __popc(live & below(j + G));
-            const int32_t adA = bp4 + ((aliveA ? __popc(live & below(j)) : G - 1) << 2);
-            const int32_t adL = bp4 + (((aliveB && dB < G) ? dB : (nn < G ? G - 1 : 0)) << 2);
-            const int32_t adH = bp4 + (((aliveB && dB >= G) ? dB - G : G - 1) << 2);
-            const bool fromA = j < nA;
-            const int32_t a0 = __builtin_amdgcn_ds_permute(adA, lid), l0 = __builtin_amdgcn_ds_permute(adL, lidB);
-            const int32_t a1 = __builtin_amdgcn_ds_permute(adA, llv), l1 = __builtin_amdgcn_ds_permute(adL, llvB);
-            const int32_t a2 = __builtin_amdgcn_ds_permute(adA, lcol), l2 = __builtin_amdgcn_ds_permute(adL, lcolB);
-            lidB = __builtin_amdgcn_ds_permute(adH, lidB);
-            llvB = __builtin_amdgcn_ds_permute(adH, llvB);
-            lcolB = __builtin_amdgcn_ds_permute(adH, lcolB);
-            lid = fromA ? a0 : l0;
-            llv = fromA ? a1 : l1;
-            lcol = fromA ? a2 : l2;
+            // compaction through LDS: slot s (alive) lands at s - #dead below it
+            const bool aliveA = j < nl && !((dead >> j) & 1u), aliveB = j + G < nl && !((dead >> (j + G)) & 1u);
+            if (aliveA) {
+              const int32_t d = j - __popc(dead & below(j));
+              comp[d] = lid;
+              comp[16 + d] = llv;
+              comp[32 + d] = lcol;
+            }
+            if (aliveB) {
+              const int32_t d = j + G - __popc(dead & below(j + G));
+              comp[d] = lidB;
+              comp[16 + d] = llvB;
+              comp[32 + d] = lcolB;
+            }
+            __builtin_amdgcn_wave_barrier();
+            lid = comp[j];
+            llv = comp[16 + j];
+            lcol = comp[32 + j];
+            lidB = comp[G + j];
+            llvB = comp[16 + G + j];
+            lcolB = comp[32 + G + j];
+            __builtin_amdgcn_wave_barrier();
             nl -= __popc(dead);
           }
         }
