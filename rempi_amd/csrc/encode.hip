@@ -1033,7 +1033,7 @@ __global__ void __launch_bounds__(256) k_pos_rows(const Unit* __restrict__ units
 // the IGNORE of a chain column j (row r = inv[j], Kr(r) = Kc(j)) at r + j - Kc, right after
 // the REMOVEs of its gap: every entry of the sequence comes from this pass.
 //
-// The entries of a round of 1024 columns land within a few dozen positions of one contiguous
+// The entries of a round of columns land within a few dozen positions of one contiguous
 // stretch of the sequence (the REMOVE / IGNORE positions ascend with the column, the ADDs of
 // the same rows fill the gaps between them), but each one is a single word: stored one by
 // one, every store instruction touches a dozen lines and the lines go to memory several times
@@ -1046,8 +1046,11 @@ __global__ void __launch_bounds__(256) k_pos_cols(const Unit* __restrict__ units
                                                   const uint8_t* __restrict__ chain, const int32_t* __restrict__ posA,
                                                   const int32_t* __restrict__ crow, uint32_t* __restrict__ seq,
                                                   int32_t* __restrict__ sx) {
-  constexpr int32_t CAP = 2560;   // positions of the image (a round makes ~1.6 K entries)
-  constexpr int32_t SLACK = 256;  // of them, before the round's first REMOVE / IGNORE position
+  // (rounds of 512 columns: half the LDS of 1024-column rounds, which matters beside the other
+  // lanes' kernels, at the same time alone)
+  constexpr int32_t PER = 2, ROUND = 256 * PER;
+  constexpr int32_t CAP = 2 * ROUND + 256;  // positions of the image (a round makes ~0.8 K entries)
+  constexpr int32_t SLACK = 192;  // of them, before the round's first REMOVE / IGNORE position
   constexpr uint32_t kNone = 3u;  // no entry has type 3
   __shared__ int32_t lds[4];
   __shared__ uint32_t wseq[CAP];
@@ -1058,7 +1061,7 @@ __global__ void __launch_bounds__(256) k_pos_cols(const Unit* __restrict__ units
   uint32_t* sq = seq + 2 * a;
   int32_t* sxa = sx + 2 * a;
   int32_t ck = 0;
-  for (int32_t b = 0; b < M; b += 1024) {
+  for (int32_t b = 0; b < M; b += ROUND) {
     const int32_t base = ((ck < K) ? crow[a + ck] : M) + b - ck - SLACK;  // position of image slot 0
     for (int32_t z = threadIdx.x; z < CAP; z += 256) wseq[z] = kNone;
     auto put = [&](int32_t pos, uint32_t e, int32_t x) {
@@ -1071,12 +1074,12 @@ __global__ void __launch_bounds__(256) k_pos_cols(const Unit* __restrict__ units
         if ((e & 3u) != kIgn) sxa[pos] = x;
       }
     };
-    const int32_t j0 = b + 4 * threadIdx.x;
-    int32_t row[4];
-    bool isc[4];
+    const int32_t j0 = b + PER * threadIdx.x;
+    int32_t row[PER];
+    bool isc[PER];
     int32_t v = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < PER; q++) {
       const bool ok = j0 + q < M;
       row[q] = ok ? inv[a + j0 + q] : 0;
       isc[q] = !ok || chain[a + row[q]];
@@ -1085,7 +1088,7 @@ __global__ void __launch_bounds__(256) k_pos_cols(const Unit* __restrict__ units
     int32_t tot;
     int32_t kc = ck + block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);  // (barriers: the image is cleared)
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < PER; q++) {
       const int32_t j = j0 + q;
       if (isc[q]) {
         if (j < M) put(row[q] + j - kc, kIgn, 0);
@@ -1132,13 +1135,16 @@ __device__ __forceinline__ int32_t delta_word(uint32_t e) {
 
 __global__ void __launch_bounds__(256, 7) k_deltas(const Unit* __restrict__ units, const uint32_t* __restrict__ seq,
                                                    const int32_t* __restrict__ sx, uint8_t* __restrict__ out) {
-  // LDS and registers are kept small (20.5 KB, <= 72 VGPRs) so that 7 blocks share a CU.
-  constexpr int32_t RING = 2048;  // the last RING sequence entries, for the span counts
+  // LDS and registers are kept small (10.3 KB, <= 72 VGPRs): beside the other lanes' kernels the
+  // LDS left on a CU decides how many blocks run.  Rounds of ROUND sequence entries, PER per thread.
+  constexpr int32_t PER = 2, ROUND = 256 * PER;
+  constexpr int32_t RING = 2 * ROUND;  // the last RING sequence entries, for the span counts
   constexpr int32_t kLongSpan = 192;
+  static_assert(RING - ROUND > kLongSpan, "a short span must lie in the ring");
   __shared__ int32_t lds[4];
-  __shared__ int2 items[1024];  // second occurrences of the round: {position s, entry}, then {s, delta}
+  __shared__ int2 items[ROUND];  // second occurrences of the round: {position s, entry}, then {s, delta}
   __shared__ int32_t ring[RING];
-  __shared__ int32_t longs[1024];  // items of the round with long spans; then the ids of the round's pairs
+  __shared__ int32_t longs[ROUND];  // items of the round with long spans; then the ids of the round's pairs
   __shared__ int32_t nlong;
   __shared__ int32_t carry[4];     // the last two ids and the last two deltas before this round (LP)
   const Unit u = units[blockIdx.x];
@@ -1154,33 +1160,33 @@ __global__ void __launch_bounds__(256, 7) k_deltas(const Unit* __restrict__ unit
   if (threadIdx.x < 4) carry[threadIdx.x] = 0;
   // this round's sequence entries; the next round's are loaded while the spans of this one
   // are counted
-  uint32_t e[4];
+  uint32_t e[PER];
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const int32_t z = 4 * threadIdx.x + q;
+  for (int q = 0; q < PER; q++) {
+    const int32_t z = PER * threadIdx.x + q;
     e[q] = (z < L) ? sq[z] : kIgn;
   }
-  for (int32_t b = 0; b < L; b += 1024) {
-    const int32_t q0 = b + 4 * threadIdx.x;
+  for (int32_t b = 0; b < L; b += ROUND) {
+    const int32_t q0 = b + PER * threadIdx.x;
     int32_t v = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++)
+    for (int q = 0; q < PER; q++)
       if ((e[q] & 3) != kIgn && (int32_t)(e[q] >> 2) < q0 + q) v++;
     int32_t tot;
     int32_t k = block_exclusive_scan<256>(v, 0, OpAdd(), lds, &tot);
     if (threadIdx.x == 0) nlong = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < PER; q++) {
       ring[(q0 + q) & (RING - 1)] = delta_word(e[q]);
       if ((e[q] & 3) != kIgn && (int32_t)(e[q] >> 2) < q0 + q) items[k++] = make_int2(q0 + q, (int32_t)e[q]);
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int32_t z = q0 + 1024 + q;
+    for (int q = 0; q < PER; q++) {
+      const int32_t z = q0 + ROUND + q;
       e[q] = (z < L) ? sq[z] : kIgn;
     }
-    const int32_t rlo = b + 1024 - RING;  // entries >= rlo are in the ring
+    const int32_t rlo = b + ROUND - RING;  // entries >= rlo are in the ring
     for (int32_t it = threadIdx.x; it < tot; it += 256) {
       const int2 item = items[it];
       const int32_t s = item.x, f = (int32_t)((uint32_t)item.y >> 2);
@@ -1197,7 +1203,7 @@ __global__ void __launch_bounds__(256, 7) k_deltas(const Unit* __restrict__ unit
       items[it].y = (((uint32_t)item.y & 3) == kRem) ? -d : d;
     }
     __syncthreads();
-    // long spans, and spans that reach behind the ring (entries older than ~1 K come from
+    // long spans, and spans that reach behind the ring (entries more than half a ring back come from
     // memory): one wave per item
     for (int32_t li = wave_id(); li < nlong; li += 4) {
       const int32_t it = longs[li];
