@@ -42,7 +42,11 @@ namespace cdcx {
 
 namespace {
 constexpr int G8 = 8;
-constexpr int kRing8 = 32;      // rows of {par, column} per group in LDS
+// Rows of {par, column} per group in LDS.  Five blocks per CU hold their rings for the whole
+// kernel, and the LDS they leave decides how many blocks of the other streams' kernels run beside
+// them: with 64 rows (27.6 KB per block) this kernel and everything next to it ran a third slower.
+// Climbs in near-sorted traces stay within 32 rows; older rows are read from memory.
+constexpr int kRing8 = 32;
 constexpr int kTopRing = 32;    // spilled tops per group in LDS: one 128-byte line of topg
 constexpr int kQBuf = 8;        // max-level rows per group kept in LDS until the segment ends
 
