@@ -41,6 +41,10 @@ KERNEL(k_salu, asm volatile("s_add_u32 %0, %0, 1" : "+s"(sd) : : "scc");)
 KERNEL(k_lshl_add, asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(a) : "v"(b));)
 KERNEL(k_add3, asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));)
 KERNEL(k_lshl_add64, asm volatile("v_lshl_add_u64 %0, %0, 2, %1" : "+v"(q) : "v"(q));)
+KERNEL(k_cmp64, asm volatile("v_cmp_lt_u64 vcc, %0, %1" : : "v"(q), "v"(q) : "vcc");)
+KERNEL(k_cmp64_addc, asm volatile("v_cmp_lt_u64 vcc, %1, %1\n v_addc_co_u32 %0, vcc, 0, %0, vcc" : "+v"(a) : "v"(q) : "vcc");)
+KERNEL(k_cmp32_addc, asm volatile("v_cmp_lt_u32 vcc, %1, %1\n v_addc_co_u32 %0, vcc, 0, %0, vcc" : "+v"(a) : "v"(b) : "vcc");)
+KERNEL(k_ds_read64, asm volatile("ds_read_b64 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(q) : "v"(b));)
 
 int main() {
   int* out;
@@ -61,7 +65,9 @@ int main() {
       {"v_cmp -> vcc", k_cmp_vcc, 1}, {"v_cmp -> sgpr pair", k_cmp_sgpr, 1}, {"v_cmp + s_and (pair)", k_cmp_sand, 1},
       {"v_cmp + v_cndmask (pair)", k_cmp_use, 1}, {"v_readlane", k_readlane, 1}, {"v_ffbl_b32", k_ffbl, 1},
       {"ds_bpermute + wait", k_bperm, 1}, {"ds_bpermute (no wait)", k_bperm_nowait, 1}, {"s_add_u32", k_salu, 1},
-      {"v_lshl_add_u32", k_lshl_add, 1}, {"v_add3_u32", k_add3, 1}, {"v_lshl_add_u64", k_lshl_add64, 1}};
+      {"v_lshl_add_u32", k_lshl_add, 1}, {"v_add3_u32", k_add3, 1}, {"v_lshl_add_u64", k_lshl_add64, 1},
+      {"v_cmp_lt_u64 -> vcc", k_cmp64, 1}, {"v_cmp_lt_u64 + v_addc (pair)", k_cmp64_addc, 1},
+      {"v_cmp_lt_u32 + v_addc (pair)", k_cmp32_addc, 1}, {"ds_read_b64 + wait", k_ds_read64, 1}};
   for (auto& k : ks) {
     for (int wpsimd : {1, 2, 8}) {
       const int blocks = cus * wpsimd;  // 256 threads = 4 waves = one per SIMD of a CU
