@@ -327,3 +327,29 @@ def test_chain_stitching_shapes_vs_oracle(kind):
             elif c.decode_stream(got) != O.decode(want):
                 bad.append((t, which, len(perm), "tables"))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("n_sets", [17, 64, 200, 256])
+def test_many_tables_vs_oracle(n_sets):
+    """Ranks with many matching sets: table indexes of up to eight bits in the scatter's ballots,
+    the high rows of its slot table and of the tile histograms, hundreds of units per chunk."""
+    rng = np.random.default_rng(4000 + n_sets)
+    bad = []
+    for t, mx in enumerate((131072, 131072, 700)):
+        ids = sorted(int(x) for x in rng.choice(256, size=n_sets, replace=False))
+        recs = S.gen_stream(int(rng.integers(1 << 30)), int(rng.integers(2000, 6000)), n_senders=n_sets + int(rng.integers(0, 20)),
+                            set_ids=ids, jitter=6)
+        want, _ = O.encode(recs, mx)
+        got = ctx(mx).encode_stream(recs)
+        if got != want:
+            bad.append((t, mx, recs.shape[0], first_diff(got, want)))
+        elif ctx(mx).decode_stream(got) != O.decode(want):
+            bad.append((t, mx, "tables"))
+    assert not bad, bad
+
+
+def test_set_id_out_of_range():
+    """matching_set_id 256 is past the library's limit: an error, not a wrong file."""
+    recs = S.gen_stream(11, 500, n_senders=6, set_ids=[0, 3, 256])
+    with pytest.raises(cdcx.CdcxError):
+        ctx(131072).encode_stream(recs)
