@@ -550,6 +550,7 @@ __device__ __forceinline__ bool window_rank_try(const Unit& u, int32_t t0, int l
 #pragma unroll
     for (int j = e; j < 4; j++) cnt[j] += v < own[j] ? 1 : 0;
   }
+  __syncthreads();  // (rk shares its storage with xk: every thread is done with the keys)
 #pragma unroll
   for (int j = 0; j < 4; j++) rk[L + j] = t0 + L + j - D + cnt[j];
   return __syncthreads_or(bad);
@@ -591,7 +592,8 @@ __global__ void __launch_bounds__(256) k_window_rank(Unit* __restrict__ units, c
                                                      int32_t* __restrict__ inv, uint64_t* __restrict__ skey) {
   constexpr int NX = 2 * kRankNarrow + 1 + kSortTile + kRankNarrow;
   __shared__ uint64_t xk[NX + NX / 4 + 1];
-  __shared__ int32_t rk[kSortTile];
+  int32_t* rk = reinterpret_cast<int32_t*>(xk);  // the tile's ranks, once the keys are no longer needed
+  static_assert(sizeof(xk) >= kSortTile * sizeof(int32_t), "the ranks fit the key storage");
   const SortTile w = st[blockIdx.x];
   if (w.unit < 0) return;  // past the batch's sort tiles (the grid is an upper bound)
   const Unit u = units[w.unit];
@@ -606,7 +608,7 @@ __global__ void __launch_bounds__(256) k_window_rank_wide(Unit* __restrict__ uni
                                                           uint64_t* __restrict__ skey) {
   constexpr int NX = 2 * kRankWin + 1 + kSortTile + kRankWin;
   __shared__ uint64_t xk[NX + NX / 4 + 1];
-  __shared__ int32_t rk[kSortTile];
+  int32_t* rk = reinterpret_cast<int32_t*>(xk);  // the tile's ranks, once the keys are no longer needed
   const Unit u = units[blockIdx.x];
   if (!(u.wfail & 4)) return;
   bool bad = false;
