@@ -33,7 +33,7 @@ enum KernelId {
   K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_RANK_SCAN,
   K_CHUNKS, K_UNITS_LB, K_LISTS, K_UNIT_PREP, K_WINDOW_RANK, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_G8, K_CHAIN_G16, K_CHAIN_G64, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
   K_WRITE_UNITS, K_CHUNK_HEADERS, K_FOOTER_ORDER, K_FOOTER_WRITE, K_WRITE_KEYS,
-  K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS, K_DEC_PACK, K_VERIFY,
+  K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_PAIRS, K_DEC_SEG, K_DEC_CHECK, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS, K_DEC_PACK, K_VERIFY,
   K_GEN_TILE_SUMS, K_GEN_RANK_SCAN, K_GEN_FRAMES, K_GEN_AKEYS, K_GEN_ARRIVAL, K_GEN_RECORDS,
   K_COUNT
 };
@@ -41,7 +41,7 @@ const char* kKernelNames[K_COUNT] = {
   "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_rank_scan",
   "k_chunks", "k_units_lb", "k_lists", "k_unit_prep", "k_window_rank", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp8", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
-  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records", "k_dec_pack_tables", "k_verify_roundtrip",
+  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_pair_scan", "k_dec_perm_seg", "k_dec_perm_check", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records", "k_dec_pack_tables", "k_verify_roundtrip",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
 
 struct HipError {
@@ -198,8 +198,8 @@ struct cdcx_ctx {
   bool chain_stats = getenv("CDCX_CHAIN_STATS") != nullptr;
   // First chain tier (diagnostics / tests): 0 = 16-lane groups, 1 = 64-lane groups, 2 = lane kernel.
   int chain_tier = getenv("CDCX_CHAIN_TIER") ? atoi(getenv("CDCX_CHAIN_TIER")) : 0;
-  // First permutation-rebuild tier (diagnostics / tests): 0 = 16-lane groups, 1 = 256-slot
-  // window, 2 = sequential list.
+  // First permutation-rebuild tier (diagnostics / tests): 0 = pair segments in 16-lane groups,
+  // 1 = whole units in 16-lane groups, 2 = 256-slot window, 3 = sequential list.
   int dec_tier = getenv("CDCX_DEC_TIER") ? atoi(getenv("CDCX_DEC_TIER")) : 0;
   // 1: every unit takes the tile sort (skips the windowed rank), for tests
   int rank_tier = getenv("CDCX_RANK_TIER") ? atoi(getenv("CDCX_RANK_TIER")) : 0;
@@ -782,7 +782,8 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
 // count and the error word -- a few words each -- and fetches the unit table itself only when
 // a caller asks for the decoded tables (host_dec_units).
 void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector<int64_t>& off,
-                  const std::vector<int64_t>& len, const int2* d_keys, int64_t n_keys, bool records, hipStream_t s) {
+                  const std::vector<int64_t>& len, const int2* d_keys, int64_t n_keys, bool records, bool pairs,
+                  hipStream_t s) {
   for (int r = 0; r < R; r++)
     if (off[r] & 7) throw CdcxError{CDCX_ERR_ARG, "rank files must start 8-byte aligned"};
   int64_t* d_off = c->upload("d_off", off, s);
@@ -832,7 +833,7 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   int32_t* d_rt0 = c->buf<int32_t>("d_rec_tile0", (size_t)NU + 1);
   c->launch(K_DEC_UNITS, k_dec_units, dim3(blocks(C, 64)), dim3(64), s, d_in, (const DChunk*)d_ch, C, (const int32_t*)d_fu,
             (int32_t*)nullptr, d_units, d_err);
-  c->launch(K_LISTS, k_dec_scan_units, dim3(1), dim3(kScanBlock), s, d_units, NU, (int32_t)std::min(std::max(c->dec_tier, 0), 2),
+  c->launch(K_LISTS, k_dec_scan_units, dim3(1), dim3(kScanBlock), s, d_units, NU, (int32_t)std::min(std::max(c->dec_tier, 0), 3),
             d_rt0, d_tot);
   totals();
   const int64_t wb = tot.rows, ro = tot.records, ko = tot.keys;
@@ -848,23 +849,34 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   c->dunits.clear();
   uint64_t* d_wpd = c->buf<uint64_t>(kAliasWpd, wb);
   uint64_t* d_uidd = c->buf<uint64_t>(kAliasUidd, wb);
-  uint64_t* d_idd = c->buf<uint64_t>(kAliasIdd, wb);  // written by k_dec_perm_grp
+  uint64_t* d_idd = c->buf<uint64_t>(kAliasIdd, wb);  // written by k_dec_pair_scan when somebody reads them
   uint64_t* d_dld = c->buf<uint64_t>(kAliasDld, wb);
   int32_t* d_perm = c->buf<int32_t>(kAliasPerm, ko);
   uint8_t* d_wnf = c->buf<uint8_t>(kAliasWnf, wb);
   HIPCHK(hipMemsetAsync(d_wnf, 0, wb, s));
   c->launch(K_DEC_SECTIONS, k_dec_sections, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, d_wpd, d_uidd, d_wnf,
             d_err);
-  // Permutation rebuild (decode.hip): 16-lane groups with LDS ring windows, which also invert
-  // the pair sections' LP; then the 256-slot settle-when-full window, then the sequential
-  // list for whatever is left.
+  // Permutation rebuild (decode.hip).  First tier: the pair list of every unit in segments of
+  // kSegPairs pairs, one per 16-lane group -- k_dec_pair_scan inverts the pair sections' LP and
+  // lays the segments out, k_dec_perm_seg replays them, k_dec_perm_check compares the state every
+  // segment started from with the state its predecessor ended in.  Units that do not pass go,
+  // whole, to a 16-lane group each, then to the 256-slot settle-when-full window, then to the
+  // sequential list.
+  const int64_t nsegs = tot.segs;
   int32_t* d_cinv = c->buf<int32_t>(kAliasCinv, ko);
-  int32_t* d_nfail = c->buf<int32_t>("d_nfail", 2);
-  HIPCHK(hipMemsetAsync(d_nfail, 0, 8, s));
-  int32_t* d_order = c->buf<int32_t>("d_perm_order", NU);
-  c->launch(K_LISTS, k_dec_order, dim3(blocks(NU, 256)), dim3(256), s, (const DUnit*)d_units, NU, d_order);
-  c->launch_gated(1, NU >= 4096, K_DEC_WIN1, k_dec_perm_grp, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order, NU, d_in,
-            d_idd, d_dld, d_perm, d_cinv, d_nfail);
+  int32_t* d_nfail = c->buf<int32_t>("d_nfail", 4);
+  HIPCHK(hipMemsetAsync(d_nfail, 0, 16, s));
+  DSeg* d_segs = c->buf<DSeg>("d_segs", nsegs);
+  int64_t* d_pcar = c->buf<int64_t>("d_pcar", 4 * nsegs);
+  int32_t* d_dump_t = c->buf<int32_t>("d_dump_t", (size_t)nsegs * kSegWin);
+  int32_t* d_dump_w = c->buf<int32_t>("d_dump_w", (size_t)nsegs * kSegWin);
+  c->launch(K_DEC_PAIRS, k_dec_pair_scan, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, 1 | (pairs ? 4 : 0), d_segs,
+            d_pcar, d_idd, d_dld);
+  c->launch_gated(1, NU >= 4096, K_DEC_SEG, k_dec_perm_seg<true>, dim3(blocks(nsegs, 4)), dim3(64), s, d_units,
+                  (const int32_t*)nullptr, (const DSeg*)d_segs, nsegs, 0, d_in, (const int64_t*)d_pcar, d_perm, d_cinv,
+                  d_dump_t, d_dump_w, d_nfail);
+  c->launch(K_DEC_CHECK, k_dec_perm_check, dim3(blocks(nsegs, 8)), dim3(256), s, d_units, (const DSeg*)d_segs, nsegs,
+            (const int32_t*)d_dump_t, (const int32_t*)d_dump_w, d_nfail);
   // The record tiles are listed while the rebuild runs; the reconstruction itself is launched
   // before the wait for the failure count when no unit can have failed into a later tier.
   int4* d_rt = nullptr;
@@ -886,17 +898,27 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
     if (c->dec_tier <= 0) nf = *reinterpret_cast<const int32_t*>(h + o);
   }
   if (nf > 0) {
-    c->launch(K_DEC_WIN4, k_dec_perm_window<4>, dim3(NU), dim3(64), s, d_units, NU, 1, (const uint64_t*)d_idd,
-              (const uint64_t*)d_dld, d_perm, d_nfail + 1);
-    const int32_t nf2 = c->dec_tier > 1 ? NU : c->download(d_nfail + 1, 1, s)[0];
-    if (nf2 > 0) {
-      int32_t* d_nx = c->buf<int32_t>("d_nx", wb);  // the sequential list only exists when needed
-      int32_t* d_pv = c->buf<int32_t>("d_pv", wb);
-      c->launch(K_DEC_PERM, k_dec_perm_lane, dim3(blocks(NU, 64)), dim3(64), s, (const DUnit*)d_units, NU,
-                (const uint64_t*)d_idd, (const uint64_t*)d_dld, d_nx, d_pv, d_perm, d_err);
+    if (!pairs)  // the later tiers read the decoded pair arrays
+      c->launch(K_DEC_PAIRS, k_dec_pair_scan, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, 2, (DSeg*)nullptr,
+                (int64_t*)nullptr, d_idd, d_dld);
+    int32_t* d_order = c->buf<int32_t>("d_perm_order", NU);
+    c->launch(K_LISTS, k_dec_order, dim3(blocks(NU, 256)), dim3(256), s, (const DUnit*)d_units, NU, d_order);
+    c->launch(K_DEC_WIN1, k_dec_perm_seg<false>, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order,
+              (const DSeg*)nullptr, (int64_t)NU, 1, d_in, (const int64_t*)nullptr, d_perm, d_cinv, (int32_t*)nullptr,
+              (int32_t*)nullptr, d_nfail + 1);
+    const int32_t nf1 = c->dec_tier > 1 ? NU : c->download(d_nfail + 1, 1, s)[0];
+    if (nf1 > 0) {
+      c->launch(K_DEC_WIN4, k_dec_perm_window<4>, dim3(NU), dim3(64), s, d_units, NU, 2, (const uint64_t*)d_idd,
+                (const uint64_t*)d_dld, d_perm, d_nfail + 2);
+      const int32_t nf2 = c->dec_tier > 2 ? NU : c->download(d_nfail + 2, 1, s)[0];
+      if (nf2 > 0) {
+        int32_t* d_nx = c->buf<int32_t>("d_nx", wb);  // the sequential list only exists when needed
+        int32_t* d_pv = c->buf<int32_t>("d_pv", wb);
+        c->launch(K_DEC_PERM, k_dec_perm_lane, dim3(blocks(NU, 64)), dim3(64), s, (const DUnit*)d_units, NU,
+                  (const uint64_t*)d_idd, (const uint64_t*)d_dld, d_nx, d_pv, d_perm, d_err);
+      }
     }
     c->launch(K_DEC_PERM, k_dec_cinv, dim3(NU), dim3(256), s, (const DUnit*)d_units, (const int32_t*)d_perm, d_cinv);
-    nf = nf2;
     c->check_err(d_err, s);
   }
   c->last_fallback_units = nf;
@@ -1276,7 +1298,7 @@ int cdcx_decode_stream(cdcx_ctx* c, const uint8_t* in, size_t len, uint8_t** dum
     hipStream_t s = c->stream;
     uint8_t* d = c->buf<uint8_t>("h_file", len);
     if (len) HIPCHK(hipMemcpyAsync(d, in, len, hipMemcpyHostToDevice, s));
-    decode_batch(c, 1, d, {0}, {(int64_t)len}, nullptr, 0, false, s);
+    decode_batch(c, 1, d, {0}, {(int64_t)len}, nullptr, 0, false, true, s);
     std::vector<int64_t> t = tables_dump(c, in, s);
     *dump = reinterpret_cast<uint8_t*>(host_copy(t));
     *dump_len = t.size() * 8;
@@ -1322,7 +1344,7 @@ int cdcx_decode_chunk(cdcx_ctx* c, const uint8_t* payload, size_t len, cdcx_tabl
     hipStream_t s = c->stream;
     int64_t L = 0;
     uint8_t* d = upload_chunk_image(c, payload, len, &L, s);
-    decode_batch(c, 1, d, {0}, {L}, nullptr, 0, false, s);
+    decode_batch(c, 1, d, {0}, {L}, nullptr, 0, false, true, s);
     const DecodedTables t = download_tables(c, s);
     // test_tables_map: ascending set id, the last table of an id wins
     std::map<int32_t, int32_t> bysid;
@@ -1394,7 +1416,7 @@ int cdcx_reconstruct_chunk(cdcx_ctx* c, const uint8_t* payload, size_t len, cons
     uint8_t* d = upload_chunk_image(c, payload, len, &L, s);
     int2* dk = c->buf<int2>("h_keys", n_keys);
     if (n_keys) HIPCHK(hipMemcpyAsync(dk, keys, 8 * n_keys, hipMemcpyHostToDevice, s));
-    decode_batch(c, 1, d, {0}, {L}, dk, (int64_t)n_keys, true, s);
+    decode_batch(c, 1, d, {0}, {L}, dk, (int64_t)n_keys, true, false, s);
     std::vector<int32_t> r = c->download(c->d_rec_out, 8 * c->n_rec_out, s);
     *rec8 = host_copy(r);
     *n_out = (size_t)c->n_rec_out;
@@ -1453,7 +1475,7 @@ int cdcx_reconstruct_stream(cdcx_ctx* c, const uint8_t* in, size_t len, const in
     if (len) HIPCHK(hipMemcpyAsync(d, in, len, hipMemcpyHostToDevice, s));
     int2* dk = c->buf<int2>("h_keys", n_keys);
     if (n_keys) HIPCHK(hipMemcpyAsync(dk, keys, 8 * n_keys, hipMemcpyHostToDevice, s));
-    decode_batch(c, 1, d, {0}, {(int64_t)len}, dk, (int64_t)n_keys, true, s);
+    decode_batch(c, 1, d, {0}, {(int64_t)len}, dk, (int64_t)n_keys, true, false, s);
     std::vector<int32_t> r = c->download(c->d_rec_out, 8 * c->n_rec_out, s);
     *rec8 = host_copy(r);
     *n_out = (size_t)c->n_rec_out;
@@ -1495,7 +1517,7 @@ int cdcx_decode_batch_device(cdcx_ctx* c, int32_t n_ranks, const uint8_t* d_in, 
     return CDCX_ERR_ARG;
   return guarded(c, [&] {
     std::vector<int64_t> off(in_off, in_off + n_ranks), len(in_len, in_len + n_ranks);
-    decode_batch(c, n_ranks, d_in, off, len, reinterpret_cast<const int2*>(d_keys), n_keys, d_keys != nullptr,
+    decode_batch(c, n_ranks, d_in, off, len, reinterpret_cast<const int2*>(d_keys), n_keys, d_keys != nullptr, false,
                  (hipStream_t)stream);
     *d_rec_out = c->d_rec_out;
     *n_rec_out = c->n_rec_out;
@@ -1531,9 +1553,12 @@ int cdcx_decode_chunk_perm_static(cdcx_ctx* c, const uint8_t* d_payload, size_t 
   const int64_t cap = (int64_t)std::min<size_t>(perm_capacity, (size_t)kStaticMaxRows);
   hipLaunchKernelGGL(k_dec_chunk_units, dim3(1), dim3(64), 0, s, d_payload, (int64_t)len, kStaticMaxUnits, kStaticMaxRows, cap,
                      hdr, order, units);
-  hipLaunchKernelGGL(k_dec_perm_grp, dim3(kStaticMaxUnits / 4), dim3(64), 0, s, units, (const int32_t*)order, kStaticMaxUnits,
-                     d_payload, idd, dld, d_perm, cinv, hdr + 2);
-  hipLaunchKernelGGL(k_dec_perm_window<4>, dim3(kStaticMaxUnits), dim3(64), 0, s, units, kStaticMaxUnits, 1,
+  hipLaunchKernelGGL(k_dec_pair_scan, dim3(kStaticMaxUnits), dim3(256), 0, s, (const DUnit*)units, d_payload, 4, (DSeg*)nullptr,
+                     (int64_t*)nullptr, idd, dld);
+  hipLaunchKernelGGL(k_dec_perm_seg<false>, dim3(kStaticMaxUnits / 4), dim3(64), 0, s, units, (const int32_t*)order,
+                     (const DSeg*)nullptr, (int64_t)kStaticMaxUnits, 1, d_payload, (const int64_t*)nullptr, d_perm, cinv,
+                     (int32_t*)nullptr, (int32_t*)nullptr, hdr + 2);
+  hipLaunchKernelGGL(k_dec_perm_window<4>, dim3(kStaticMaxUnits), dim3(64), 0, s, units, kStaticMaxUnits, 2,
                      (const uint64_t*)idd, (const uint64_t*)dld, d_perm, hdr + 3);
   hipLaunchKernelGGL(k_dec_perm_lane, dim3(kStaticMaxUnits / 64), dim3(64), 0, s, (const DUnit*)units, kStaticMaxUnits,
                      (const uint64_t*)idd, (const uint64_t*)dld, nx, pv, d_perm, reinterpret_cast<uint32_t*>(hdr));
@@ -1687,7 +1712,7 @@ void replay_batch(cdcx_ctx* c, ReplayJob& job, int32_t b, hipStream_t s) {
   job.ns_read += ns_since(t);
   uint8_t* d = c->buf<uint8_t>("h_file", (size_t)std::max<int64_t>(pos, 8));
   if (pos) HIPCHK(hipMemcpyAsync(d, h, (size_t)pos, hipMemcpyHostToDevice, s));
-  decode_batch(c, R, d, off, len, nullptr, 0, false, s);
+  decode_batch(c, R, d, off, len, nullptr, 0, false, true, s);
   const DecodedTables tb = download_tables(c, s);
   job.ns_device += ns_since(t);
   job.chunks += (int64_t)c->dchunks.size();

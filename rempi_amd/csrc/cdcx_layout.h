@@ -79,8 +79,32 @@ struct DUnit {
   int64_t wbase;    // element offset into decoder scratch (sum of M + 1 over earlier units)
   int64_t rec_off;  // record offset of the unit's reconstructed stream
   int64_t key_off;  // offset of its sorted keys
-  int32_t fb;       // permutation rebuild attempt: 0 window K=1, 1 window K=4, 2 sequential
-  int32_t pad2;
+  int32_t fb;       // permutation rebuild tier the unit is at: 0 pair segments, 1 whole unit in a 16-lane
+                    // group, 2 one wave with a 256-slot window, 3 sequential list
+  int32_t nseg;     // pair segments of the unit (dec_nseg(P))
+  int64_t seg0;     // first of its segments in the batch's segment list
+};
+
+// Pair segments of the permutation rebuild (decode.hip): the pair list of a unit is cut every
+// kSegPairs pairs; a segment replays the kSegWarm pairs before its own from the untouched list
+// first, and its state then is checked against the state its predecessor ends in.
+constexpr int32_t kSegPairs = 1024;   // pairs per segment (multiple of 8 * kSegWarm)
+constexpr int32_t kSegWarm = 128;     // pairs replayed before a segment's own (multiple of 32)
+constexpr int32_t kSegDelta = 32;     // a segment's positions start this far below its smallest pair id
+constexpr int32_t kSegWin = 128;      // list positions compared between neighbouring segments (= the window)
+constexpr int32_t kSegMaxP = 262144;  // units with more pairs are rebuilt as one segment
+constexpr int32_t kSegNoCap = 0x7ffffff0;
+__host__ __device__ inline int32_t dec_nseg(int32_t P) {
+  return (P <= kSegPairs || P > kSegMaxP) ? 1 : (P + kSegPairs - 1) / kSegPairs;
+}
+struct DSeg {
+  int32_t unit;
+  int32_t s;      // ordinal within the unit
+  int32_t ka, ke; // its own pairs [ka, ke); the pairs [ka - kSegWarm, ka) are replayed first when s > 0
+  int32_t own;    // first list position the segment owns (multiple of 16; 0 for s == 0)
+  int32_t cap;    // first position of the next segment (kSegNoCap for the last one)
+  int32_t base0;  // window base at the start of the replay
+  int32_t pad;
 };
 
 
@@ -118,6 +142,7 @@ struct DecTotals {
   int64_t records;    // reconstructed records
   int64_t keys;       // sum of M
   int64_t rec_tiles;  // k_dec_records tiles
+  int64_t segs;       // pair segments (sum of dec_nseg(P))
 };
 
 struct DChunk {

@@ -156,7 +156,9 @@ __global__ void __launch_bounds__(64) k_dec_chunk_units(const uint8_t* __restric
       u.wbase = wb;
       u.rec_off = ko + q;  // not used by the permutation kernels
       u.key_off = ko;
-      u.fb = 0;
+      u.fb = 1;  // whole-unit tiers only
+      u.nseg = 1;
+      u.seg0 = q;
       wb += (int64_t)u.M + 1;
       ko += u.M;
     }
@@ -234,7 +236,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_lane(const DUnit* __restrict__ 
   const int ui = blockIdx.x * 64 + threadIdx.x;
   if (ui >= n_units) return;
   const DUnit u = units[ui];
-  if (u.fb != 2) return;  // rebuilt by k_dec_perm_window
+  if (u.fb != 3) return;  // rebuilt by an earlier tier
   const int32_t M = u.M;
   int32_t* n = nx + u.wbase;
   int32_t* p = pv + u.wbase;
@@ -450,7 +452,145 @@ template __global__ void k_dec_perm_window<2>(DUnit*, int32_t, int32_t, const ui
 template __global__ void k_dec_perm_window<4>(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);
 
 // ---------------------------------------------------------------------------------------
-// Permutation rebuild, first attempt: one unit per 16-lane group (four units per wave).
+// Pair sections of every unit in one pass, one workgroup per unit: the inverse linear
+// prediction of ids and delays (x = prefix(prefix(y)) of the sign-extended int32 words, mod
+// 2^64, decode :1004-1014 + rempi_compression_util.cpp:157-168), and from it
+//   mode & 1: the unit's pair segments (DSeg) -- the prediction state at the first replayed pair
+//             of every segment (pcar: z, x of ids, z, x of delays before that pair) and the list
+//             positions each segment owns, from the suffix minima of the ids;
+//   mode & 2: the decoded pair arrays of the units that left the first tier (fb != 0);
+//   mode & 4: the decoded pair arrays of every unit (table dumps).
+namespace {
+// exclusive prefix sums of two words over the 256 threads (wsum: [4][4] words of LDS)
+__device__ __forceinline__ void block_scan2(uint64_t a, uint64_t b, uint64_t (*wsum)[4], uint64_t* ea, uint64_t* eb,
+                                            uint64_t* ta, uint64_t* tb) {
+  const int w = threadIdx.x >> 6;
+  const uint64_t ia = wave_inclusive_scan(a, OpAdd()), ib = wave_inclusive_scan(b, OpAdd());
+  __syncthreads();  // (the previous call's readers are done)
+  if (lane_id() == kWave - 1) {
+    wsum[w][0] = ia;
+    wsum[w][1] = ib;
+  }
+  __syncthreads();
+  uint64_t pa = 0, pb = 0, sa = 0, sb = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint64_t va = wsum[q][0], vb = wsum[q][1];
+    if (q < w) {
+      pa += va;
+      pb += vb;
+    }
+    sa += va;
+    sb += vb;
+  }
+  *ea = pa + ia - a;
+  *eb = pb + ib - b;
+  *ta = sa;
+  *tb = sb;
+}
+__device__ __forceinline__ int32_t seg_floor(int32_t min_id) { return max(0, min_id - kSegDelta) & ~15; }
+}  // namespace
+
+__global__ void __launch_bounds__(256) k_dec_pair_scan(const DUnit* __restrict__ units, const uint8_t* __restrict__ in,
+                                                       int32_t mode, DSeg* __restrict__ segs, int64_t* __restrict__ pcar,
+                                                       uint64_t* __restrict__ idd, uint64_t* __restrict__ dld) {
+  __shared__ int32_t bmin[kSegMaxP / kSegWarm + 1];  // smallest id of every kSegWarm pairs, then suffix minima
+  __shared__ uint64_t wsum[4][4];
+  const int32_t ui = blockIdx.x;
+  const DUnit u = units[ui];
+  const int32_t P = u.P, tid = threadIdx.x;
+  const bool lists = (mode & 1) && u.nseg > 1;  // (more than one segment: P <= kSegMaxP)
+  const bool store = (mode & 4) || ((mode & 2) && u.fb != 0);
+  if ((mode & 1) && u.nseg <= 1 && tid == 0)
+    segs[u.seg0] = DSeg{ui, 0, 0, P, 0, kSegNoCap, 0, 0};
+  if (!lists && !store) return;
+  const int32_t* yid = reinterpret_cast<const int32_t*>(in + u.pair_off);
+  const int32_t* ydl = yid + P;
+  uint64_t czi = 0, cxi = 0, czd = 0, cxd = 0;  // z, x before the tile's first pair
+  for (int32_t t0 = 0; t0 < P; t0 += 1024) {
+    const int32_t k = t0 + 4 * tid;
+    uint64_t zi[4], zd[4], s2i = 0, s2d = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const bool inb = k + q < P;
+      const uint64_t yi = inb ? sext(yid[k + q]) : 0, yd = inb ? sext(ydl[k + q]) : 0;
+      zi[q] = (q ? zi[q - 1] : 0) + yi;
+      zd[q] = (q ? zd[q - 1] : 0) + yd;
+      s2i += zi[q];
+      s2d += zd[q];
+    }
+    uint64_t zoi, zod, tzi, tzd, xoi, xod, txi, txd;
+    block_scan2(zi[3], zd[3], wsum, &zoi, &zod, &tzi, &tzd);
+    block_scan2(4 * zoi + s2i, 4 * zod + s2d, wsum, &xoi, &xod, &txi, &txd);
+    const uint64_t z0i = czi + zoi, z0d = czd + zod;
+    uint64_t xi = cxi + 4 * czi * (uint64_t)tid + xoi, xd = cxd + 4 * czd * (uint64_t)tid + xod;
+    if (lists && (k & (kSegWarm - 1)) == 0 && ((k / kSegWarm) & 7) == 7) {  // k = s * kSegPairs - kSegWarm
+      const int32_t sg = (k / kSegWarm + 1) >> 3;
+      if (sg < u.nseg) {
+        int64_t* o = pcar + 4 * (u.seg0 + sg);
+        o[0] = (int64_t)z0i;
+        o[1] = (int64_t)xi;
+        o[2] = (int64_t)z0d;
+        o[3] = (int64_t)xd;
+      }
+    }
+    int32_t mn = INT32_MAX;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      xi += z0i + zi[q];
+      xd += z0d + zd[q];
+      if (k + q < P) {
+        if (store) {
+          idd[u.wbase + k + q] = xi;
+          dld[u.wbase + k + q] = xd;
+        }
+        mn = min(mn, (int32_t)xi);
+      }
+    }
+    if (lists) {
+#pragma unroll
+      for (int dlt = 16; dlt >= 1; dlt >>= 1) mn = min(mn, __shfl_xor(mn, dlt, 64));
+      if ((tid & 31) == 0) bmin[(t0 >> 7) + (tid >> 5)] = mn;
+    }
+    cxi += 1024 * czi + txi;
+    cxd += 1024 * czd + txd;
+    czi += tzi;
+    czd += tzd;
+  }
+  if (!lists) return;
+  __syncthreads();
+  const int32_t nb = (P + kSegWarm - 1) / kSegWarm;
+  if (tid < kWave) {  // suffix minima, 64 entries at a time from the top
+    int32_t carry = INT32_MAX;
+    for (int32_t hi = nb; hi > 0; hi -= kWave) {
+      const int32_t idx = hi - 1 - tid;
+      int32_t v = idx >= 0 ? bmin[idx] : INT32_MAX;
+      v = min(wave_inclusive_scan(v, OpMin()), carry);
+      if (idx >= 0) bmin[idx] = v;
+      carry = __shfl(v, kWave - 1, kWave);
+    }
+  }
+  __syncthreads();
+  for (int32_t sg = tid; sg < u.nseg; sg += 256) {
+    const int32_t ka = sg * kSegPairs;
+    DSeg d;
+    d.unit = ui;
+    d.s = sg;
+    d.ka = ka;
+    d.ke = min(P, ka + kSegPairs);
+    d.own = sg ? seg_floor(bmin[ka / kSegWarm]) : 0;
+    d.cap = sg + 1 < u.nseg ? min(kSegNoCap, seg_floor(bmin[(ka + kSegPairs) / kSegWarm])) : kSegNoCap;
+    d.base0 = sg ? seg_floor(bmin[(ka - kSegWarm) / kSegWarm]) : 0;
+    d.pad = 0;
+    segs[u.seg0 + sg] = d;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Permutation rebuild in 16-lane groups (four per wave): one pair segment per group (SEG, the
+// first tier) or one whole unit per group (the second tier, for units whose segments did not
+// check out).
+//
 // The list is held as a window of list positions [base, base + W) in a per-group LDS ring,
 // plus an LDS map element -> position for the elements in the window.  Every position at
 // or past the window still holds its initial element (position q holds q): nothing has
@@ -463,18 +603,29 @@ template __global__ void k_dec_perm_window<4>(DUnit*, int32_t, int32_t, const ui
 // Why groups: with one unit per wave the per-pair control is scalar code (~40 SALU per
 // pair) and the scalar unit is shared by the CU's four SIMDs, so that version is bound by
 // scalar issue; here the per-pair control is group-uniform vector code shared by four
-// units.  All groups consume one pair per step (the pair index is the step count), so the
-// q-th pair of a 16-pair batch is broadcast from group lane q with DPP row_newbcast.  Units
-// are handed out longest-first (`order`) so that the four units of a wave finish together.
-// The pair sections' inverse LP (two chained prefix sums) is done here, 16 pairs at a time.
+// groups.  All groups consume one pair per step (the pair index is the step count), so the
+// q-th pair of a 16-pair batch is broadcast from group lane q with DPP row_newbcast.
+//
+// Segments.  One unit's pair list is one dependency chain (17 K pairs in the bench traces),
+// and a batch has too few units to fill the GPU with such chains.  But a move only touches
+// the list near its id, and ids rise along the pair list, so the state a stretch of pairs
+// meets depends on the pairs shortly before it only.  A segment therefore starts from the
+// untouched list, replays the kSegWarm pairs before its own without writing anything (a pair
+// that does not fit the window is skipped there), moves its window to the first position it
+// owns (`own`) and writes the kSegWin positions from there to dumpW.  Its predecessor never
+// slides past that position (`cap`) and writes the same positions of its final state to
+// dumpT; behind them both lists are untouched.  k_dec_perm_check compares the two: where they
+// agree the segment started from the list the sequential replay has at that pair, and since it
+// fails (like the whole-unit tier) on any move that reaches below its window, everything it
+// wrote is what the sequential replay writes.  A unit with a failed or disagreeing segment
+// goes to the next tier whole; every tier rewrites all outputs of the units it takes.
 //
 // A pair that reaches behind the window, an element no longer in it, or a step past the
-// list end (the std::list wrap through its sentinel) marks the unit for the next attempt
-// (k_dec_perm_window<4>, then the sequential k_dec_perm_lane).
+// list end (the std::list wrap through its sentinel) fails the group's unit for this tier.
 namespace {
-constexpr int32_t kGW = 128;     // window slots per group (power of two)
-constexpr int32_t kGMap = 256;   // element map entries per group (power of two)
-constexpr int32_t kGAhead = 56;  // an untouched x is brought to >= kGAhead slots before the end
+constexpr int32_t kGW = kSegWin;  // window slots per group (power of two)
+constexpr int32_t kGMap = 256;    // element map entries per group (power of two)
+constexpr int32_t kGAhead = 56;   // an untouched x is brought to >= kGAhead slots before the end
 
 template <int N, int I = 0, class F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -500,10 +651,12 @@ __device__ __forceinline__ int32_t row_bcast(int32_t v) {
 }
 }  // namespace
 
-__global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, const int32_t* __restrict__ order,
-                                                     int32_t n_units, const uint8_t* __restrict__ in,
-                                                     uint64_t* __restrict__ idd, uint64_t* __restrict__ dld,
+template <bool SEG>
+__global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, const int32_t* __restrict__ order,
+                                                     const DSeg* __restrict__ segs, int64_t n_items, int32_t want_fb,
+                                                     const uint8_t* __restrict__ in, const int64_t* __restrict__ pcar,
                                                      int32_t* __restrict__ perm, int32_t* __restrict__ cinv,
+                                                     int32_t* __restrict__ dumpT, int32_t* __restrict__ dumpW,
                                                      int32_t* __restrict__ nfail) {
   constexpr int32_t W = kGW, WM = kGW - 1, MM = kGMap - 1;
   __shared__ int32_t win_all[4][W + 16];      // + one dummy slot per lane
@@ -511,38 +664,63 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
   const int g = threadIdx.x >> 4, j = threadIdx.x & 15;
   int32_t* win = win_all[g];
   int2* emap = emap_all[g];
-  const int32_t oi = blockIdx.x * 4 + g;
-  const int32_t ui = (oi < n_units) ? order[oi] : -1;
-  int32_t M = 0, P = 0;
-  int64_t wbase = 0, key_off = 0, pair_off = 0;
-  bool sim = false;  // units already marked for a later tier only get their pairs' LP inverted
+  const int64_t gi = (int64_t)blockIdx.x * 4 + g;
+  int32_t ui = -1;
+  DSeg sd{-1, 0, 0, 0, 0, kSegNoCap, 0, 0};
+  if (gi < n_items) {
+    if (SEG) {
+      sd = segs[gi];
+      ui = sd.unit;
+    } else {
+      ui = order[gi];
+    }
+  }
+  int32_t M = 0, Pu = 0;
+  int64_t key_off = 0, pair_off = 0;
+  bool sim = false;  // the group's unit is at this tier
   if (ui >= 0) {
     const DUnit& u = units[ui];
-    sim = (u.fb == 0);
+    sim = (u.fb == want_fb);
     M = u.M;
-    P = u.P;
-    wbase = u.wbase;
+    Pu = u.P;
     key_off = u.key_off;
     pair_off = u.pair_off;
+    if (!SEG) sd.ke = Pu;
   }
+  const bool wact = SEG && sim && sd.s > 0;            // replays kSegWarm pairs first
+  const bool hasn = SEG && sd.cap != kSegNoCap;        // a segment follows: leave it the final state
+  const int32_t ka = sd.ka, ke = sim ? sd.ke : sd.ka;  // the group's own pairs
+  const int32_t klo = wact ? ka - kSegWarm : ka;       // first pair it reads
+  const int32_t own = sd.own, cap = sd.cap;
   int32_t* pm = perm + key_off;
   int32_t* ci = cinv + key_off;
-  uint64_t* ip = idd + wbase;
-  uint64_t* dp = dld + wbase;
   const int32_t* yid = reinterpret_cast<const int32_t*>(in + pair_off);
-  const int32_t* ydl = yid + P;
+  const int32_t* ydl = yid + Pu;
   int64_t czi = 0, cxi = 0, czd = 0, cxd = 0;  // inverse-LP carries (rempi_compression_util.cpp:157-168)
-  for (int32_t q = j; q < W; q += 16) win[q] = q;
-  for (int32_t q = j; q < kGMap; q += 16) emap[q] = (q < W) ? make_int2(q, q) : make_int2(-1, -1);
-  int32_t base = 0;
+  if (wact) {
+    const int64_t* o = pcar + 4 * gi;
+    czi = o[0];
+    cxi = o[1];
+    czd = o[2];
+    cxd = o[3];
+  }
+  int32_t base = sd.base0;  // (a multiple of 16)
+  for (int32_t q = j; q < kGMap; q += 16) emap[q] = make_int2(-1, -1);
+  for (int32_t q = j; q < W; q += 16) {  // (entries of lane j only: in program order with the loop above)
+    const int32_t e = base + q;
+    win[e & WM] = e;
+    emap[e & MM] = make_int2(e, e);
+  }
   int32_t failv = sim ? 0 : 1;
-  const int32_t Pmax = __builtin_amdgcn_readfirstlane(wave_reduce(P, OpMax()));
-  auto slide = [&](bool go) {  // settle [base, base+16), open [base+W, base+W+16) as identity
+  auto slide = [&](auto warm_c, bool go) {  // settle [base, base+16), open [base+W, base+W+16) as identity
+    constexpr bool WARM = decltype(warm_c)::value;
     const int32_t ph = go ? ((base + j) & WM) : W + j;
     const int32_t v = win[ph];  // (dummy slot when not sliding)
-    if (go && v < M) {
-      pm[v] = base + j;
-      ci[base + j] = v;
+    if (!WARM) {
+      if (go && v < M) {
+        pm[v] = base + j;
+        ci[base + j] = v;
+      }
     }
     const int32_t e = base + W + j;
     __builtin_amdgcn_wave_barrier();
@@ -550,32 +728,38 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
     emap[go ? (e & MM) : kGMap + j] = make_int2(e, e);
     if (go) base += 16;
   };
-  // one pair of all four groups: x, d group-uniform
-  auto step = [&](int32_t k, int32_t x, int32_t d) {
+  // one pair of all four groups: x, d group-uniform.  WARM: the replay before a segment's own
+  // pairs -- the window stays at or below `own`, nothing is written, and a pair that does not
+  // fit is skipped (the state is checked afterwards).  Otherwise the window stays at or below
+  // `cap` and a pair that does not fit fails the unit.
+  auto step = [&](auto warm_c, bool in_range, int32_t x, int32_t d) {
+      constexpr bool WARM = decltype(warm_c)::value;
+      const int32_t lim = WARM ? own : cap;
       // Common path without divergent branches: predicated selects, LDS accesses of
       // inactive lanes go to per-lane dummy slots; rare cases (slides, targets past the
       // window, rotations longer than 16 slots) take wave-uniform detours.
       // (an id outside [0, M) has failed the unit when its batch was formed, in lp())
       // (flags of one step are lane masks; only the unit's failure is carried as a word)
-      bool act = (k < P) & (failv == 0);
+      bool act = in_range & (failv == 0);
       // an untouched x (at position x) is brought kGAhead slots before the window end
       const bool far = act & (x >= base + W);
       if (__builtin_amdgcn_ballot_w64(far))
-        while (__builtin_amdgcn_ballot_w64(far && x >= base + W - kGAhead)) slide(far && x >= base + W - kGAhead);
+        while (__builtin_amdgcn_ballot_w64(far && x >= base + W - kGAhead && base + 16 <= lim))
+          slide(warm_c, far && x >= base + W - kGAhead && base + 16 <= lim);
       const int2 e = emap[act ? (x & MM) : kGMap + j];
       int32_t p = e.y - base;
       int32_t t = p + d;
       const bool bad = act & ((e.x != x) | ((uint32_t)p >= (uint32_t)W) | (t < 0) | (base + t > M - 1));
-      failv |= bad ? 1 : 0;
+      if (!WARM) failv |= bad ? 1 : 0;
       act &= !bad;
       if (__builtin_amdgcn_ballot_w64(act && t > W - 1)) {
         while (__builtin_amdgcn_ballot_w64(act && t > W - 1)) {
           const bool go = act & (t > W - 1);
-          const bool stuck = go & (p < 16);
-          failv |= stuck ? 1 : 0;
+          const bool stuck = go & ((p < 16) | (base + 16 > lim));
+          if (!WARM) failv |= stuck ? 1 : 0;
           act &= !stuck;
           const bool sl = go & !stuck;
-          slide(sl);
+          slide(warm_c, sl);
           p -= sl ? 16 : 0;
           t -= sl ? 16 : 0;
         }
@@ -606,8 +790,8 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
   // low 32 bits), then the steps, each taking group lane 0 (row_newbcast:0) and shifting
   // the batch down a lane
   int32_t xs = 0, ds = 0;
-  auto lp = [&](int32_t k0, int32_t yw_i, int32_t yw_d) {
-    const bool inb = k0 + j < P;
+  auto lp = [&](auto warm_c, int32_t k0, int32_t yw_i, int32_t yw_d) {
+    constexpr bool WARM = decltype(warm_c)::value;
     const int64_t yi = (int64_t)yw_i, yd = (int64_t)yw_d;
     const int64_t zi = row_incl_scan64(yi), zd = row_incl_scan64(yd);
     const int64_t xi = cxi + (int64_t)(j + 1) * czi + row_incl_scan64(zi);
@@ -616,59 +800,116 @@ __global__ void __launch_bounds__(64) k_dec_perm_grp(DUnit* __restrict__ units, 
     czd += __shfl(zd, 15, 16);
     cxi = __shfl(xi, 15, 16);
     cxd = __shfl(xd, 15, 16);
-    if (inb) {
-      ip[k0 + j] = (uint64_t)xi;
-      dp[k0 + j] = (uint64_t)xd;
-    }
     xs = (int32_t)xi;
     ds = (int32_t)xd;
-    // an id outside [0, M) among the batch's pairs fails the unit (for this tier) at once
-    const uint64_t badm = __builtin_amdgcn_ballot_w64(inb && (uint32_t)xs >= (uint32_t)M);
-    failv |= ((badm >> (threadIdx.x & 48)) & 0xffffu) ? 1 : 0;
+    if (!WARM) {
+      // an id outside [0, M) among the batch's pairs fails the unit (for this tier) at once
+      const bool inb = k0 + j >= ka && k0 + j < ke;
+      const uint64_t badm = __builtin_amdgcn_ballot_w64(inb && (uint32_t)xs >= (uint32_t)M);
+      failv |= ((badm >> (threadIdx.x & 48)) & 0xffffu) ? 1 : 0;
+    }
   };
-  auto steps = [&](int32_t k0) {
-    const int32_t nq = min(16, Pmax - k0);
+  auto steps = [&](auto warm_c, int32_t k0, int32_t nq) {
+    constexpr bool WARM = decltype(warm_c)::value;
     for (int32_t q = 0; q < nq; q++) {
       const int32_t x = row_bcast<0>(xs), d = row_bcast<0>(ds);
       xs = __builtin_amdgcn_update_dpp(xs, xs, 0x101, 0xf, 0xf, false);  // row_shl:1
       ds = __builtin_amdgcn_update_dpp(ds, ds, 0x101, 0xf, 0xf, false);
-      step(k0 + q, x, d);
+      step(warm_c, WARM ? wact : (k0 + q < ke), x, d);
     }
   };
   // Two batches per round.  The raw words of a batch are loaded one batch ahead, and each
   // load is issued only after the previous wait (the compiler waits for all outstanding
   // memory operations at every use), so a wait never covers a load issued just before it.
-  auto ld = [&](const int32_t* y, int32_t k) { return (k + j < P) ? y[k + j] : 0; };
-  int32_t ai = ld(yid, 0), ad = ld(ydl, 0), bi = ld(yid, 16), bd = ld(ydl, 16);
-  for (int32_t k0 = 0; k0 < Pmax; k0 += 32) {
-    lp(k0, ai, ad);
-    ai = ld(yid, k0 + 32);
-    ad = ld(ydl, k0 + 32);
-    steps(k0);
-    if (k0 + 16 < Pmax) {
-      lp(k0 + 16, bi, bd);
-      bi = ld(yid, k0 + 48);
-      bd = ld(ydl, k0 + 48);
-      steps(k0 + 16);
+  auto ld = [&](const int32_t* y, int32_t k) { return (k + j >= klo && k + j < ke) ? y[k + j] : 0; };
+  const std::integral_constant<bool, true> warm_t{};
+  const std::integral_constant<bool, false> main_t{};
+  int32_t ai, ad, bi, bd;
+  if (SEG && __builtin_amdgcn_ballot_w64(wact)) {
+    const int32_t kb = ka - kSegWarm;  // (groups without a replay read nothing below ka: klo)
+    ai = ld(yid, kb), ad = ld(ydl, kb), bi = ld(yid, kb + 16), bd = ld(ydl, kb + 16);
+    for (int32_t i0 = 0; i0 < kSegWarm; i0 += 32) {
+      lp(warm_t, kb + i0, ai, ad);
+      ai = ld(yid, kb + i0 + 32);
+      ad = ld(ydl, kb + i0 + 32);
+      steps(warm_t, kb + i0, 16);
+      lp(warm_t, kb + i0 + 16, bi, bd);
+      bi = ld(yid, kb + i0 + 48);
+      bd = ld(ydl, kb + i0 + 48);
+      steps(warm_t, kb + i0 + 16, 16);
+    }
+    // the window moves up to the first owned position; the state there goes to the check
+    while (__builtin_amdgcn_ballot_w64(wact && base < own)) slide(warm_t, wact && base < own);
+    if (wact)
+      for (int32_t q = j; q < W; q += 16) dumpW[gi * W + q] = win[(base + q) & WM];
+    if (!wact) {  // (a group without a replay went through it with zero words: nothing to carry over)
+      czi = cxi = czd = cxd = 0;
+    }
+  } else {
+    ai = ld(yid, ka), ad = ld(ydl, ka), bi = ld(yid, ka + 16), bd = ld(ydl, ka + 16);
+  }
+  const int32_t imax = __builtin_amdgcn_readfirstlane(wave_reduce(ke - ka, OpMax()));
+  for (int32_t i0 = 0; i0 < imax; i0 += 32) {
+    lp(main_t, ka + i0, ai, ad);
+    ai = ld(yid, ka + i0 + 32);
+    ad = ld(ydl, ka + i0 + 32);
+    steps(main_t, ka + i0, min(16, imax - i0));
+    if (i0 + 16 < imax) {
+      lp(main_t, ka + i0 + 16, bi, bd);
+      bi = ld(yid, ka + i0 + 48);
+      bd = ld(ydl, ka + i0 + 48);
+      steps(main_t, ka + i0 + 16, min(16, imax - i0 - 16));
     }
   }
   const bool fail = failv != 0;
   if (sim && fail && j == 0) {
-    units[ui].fb = 1;
-    atomicAdd(nfail, 1);
+    if (atomicCAS(&units[ui].fb, want_fb, want_fb + 1) == want_fb) atomicAdd(nfail, 1);
   }
   if (!fail) {
+    const int32_t lim = min(M, cap);  // the positions below are this group's to write
     for (int32_t s = j; s < W; s += 16) {
       const int32_t v = win[(base + s) & WM];
-      if (v < M) {
+      if (v < M && base + s < lim) {
         pm[v] = base + s;
         ci[base + s] = v;
       }
     }
-    for (int32_t q = base + W + j; q < M; q += 16) {
+    for (int32_t q = base + W + j; q < lim; q += 16) {
       pm[q] = q;
       ci[q] = q;
     }
+    if (hasn)  // the state from `cap` on, for the next segment's check (base <= cap: the window never slid past it)
+      for (int32_t q = j; q < W; q += 16) dumpT[(gi + 1) * W + q] = (cap + q < base + W) ? win[(cap + q) & WM] : cap + q;
+  }
+}
+
+template __global__ void k_dec_perm_seg<true>(DUnit*, const int32_t*, const DSeg*, int64_t, int32_t, const uint8_t*,
+                                              const int64_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*);
+template __global__ void k_dec_perm_seg<false>(DUnit*, const int32_t*, const DSeg*, int64_t, int32_t, const uint8_t*,
+                                               const int64_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*);
+
+// The state a segment starts its own pairs from (dumpW) against the state its predecessor
+// ends in (dumpT), kSegWin list positions from the segment's first owned one; 32 lanes per
+// segment.  A difference sends the unit to the next tier.
+__global__ void __launch_bounds__(256) k_dec_perm_check(DUnit* __restrict__ units, const DSeg* __restrict__ segs,
+                                                        int64_t nsegs, const int32_t* __restrict__ dumpT,
+                                                        const int32_t* __restrict__ dumpW, int32_t* __restrict__ nfail) {
+  static_assert(kSegWin == 128, "32 lanes x int4");
+  const int64_t gi = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int l = threadIdx.x & 31;
+  bool diff = false;
+  int32_t ui = -1;
+  if (gi < nsegs) {
+    const DSeg d = segs[gi];
+    if (d.s > 0 && units[d.unit].fb == 0) {
+      ui = d.unit;
+      const int4 a = reinterpret_cast<const int4*>(dumpT)[gi * 32 + l], b = reinterpret_cast<const int4*>(dumpW)[gi * 32 + l];
+      diff = a.x != b.x || a.y != b.y || a.z != b.z || a.w != b.w;
+    }
+  }
+  const uint64_t m = __builtin_amdgcn_ballot_w64(diff);
+  if (l == 0 && ui >= 0 && ((m >> (threadIdx.x & 32)) & 0xffffffffull)) {
+    if (atomicCAS(&units[ui].fb, 0, 1) == 0) atomicAdd(nfail, 1);
   }
 }
 

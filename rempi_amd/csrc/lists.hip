@@ -282,20 +282,25 @@ __global__ void __launch_bounds__(kScanBlock) k_dec_scan_units(DUnit* __restrict
                                                                int32_t* __restrict__ tile0, DecTotals* __restrict__ tot) {
   latency_kernel();
   __shared__ int64_t lds[kScanBlock / kWave];
-  int64_t cw = 0, cr = 0, ck = 0, ct = 0;
+  int64_t cw = 0, cr = 0, ck = 0, ct = 0, cs = 0;
   for (int32_t b = 0; b < NU; b += kScanBlock) {
     const int32_t q = b + threadIdx.x;
     const bool ok = q < NU;
     int64_t M = 0, nrun = 0;
+    int32_t nseg = 0;
     if (ok) {
       M = units[q].M;
       nrun = units[q].Uc > 0 ? units[q].U : 0;
+      nseg = dec_nseg(units[q].P);
     }
     const int64_t w0 = scan_round(ok ? M + 1 : 0, cw, lds);
     const int64_t r0 = scan_round(M + nrun, cr, lds);
     const int64_t k0 = scan_round(M, ck, lds);
     const int64_t t0 = scan_round((int64_t)((ok && (M > 0 || nrun > 0)) ? max((M + kRecTile - 1) / kRecTile, (int64_t)1) : 0), ct, lds);
+    const int64_t s0 = scan_round((int64_t)nseg, cs, lds);
     if (ok) {
+      units[q].nseg = nseg;
+      units[q].seg0 = s0;
       units[q].wbase = w0;
       units[q].rec_off = r0;
       units[q].key_off = k0;
@@ -309,6 +314,7 @@ __global__ void __launch_bounds__(kScanBlock) k_dec_scan_units(DUnit* __restrict
     tot->records = cr;
     tot->keys = ck;
     tot->rec_tiles = ct;
+    tot->segs = cs;
   }
 }
 

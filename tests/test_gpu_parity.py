@@ -190,11 +190,12 @@ def test_chain_tiers_vs_oracle(tier, monkeypatch):
     c.close()
 
 
-@pytest.mark.parametrize("tier", [0, 1, 2])
+@pytest.mark.parametrize("tier", [0, 1, 2, 3])
 def test_decode_tiers_vs_oracle(tier, monkeypatch):
-    """Each permutation-rebuild tier alone (16-lane LDS-ring groups, 256-slot window,
-    sequential list) reproduces the reference tables and records, including streams whose
-    moves reach past the first tier's window (random / reversed permutations)."""
+    """Each permutation-rebuild tier alone (pair segments in 16-lane LDS-ring groups, whole units
+    in such groups, 256-slot window, sequential list) reproduces the reference tables and
+    records, including streams whose moves reach past the first tiers' window (random /
+    reversed permutations) and tables of several pair segments."""
     monkeypatch.setenv("CDCX_DEC_TIER", str(tier))
     c = rempi_amd.Context(131072)
     monkeypatch.delenv("CDCX_DEC_TIER")
@@ -202,7 +203,8 @@ def test_decode_tiers_vs_oracle(tier, monkeypatch):
     bad = []
     for t in range(40):
         mode = ["jitter", "jitter", "jitter", "reversed", "random"][t % 5]
-        recs = S.gen_stream(int(rng.integers(1 << 30)), int(rng.integers(0, 3000)), n_sets=int(rng.integers(1, 4)),
+        n = int(rng.integers(0, 3000)) if t % 4 else int(rng.integers(8000, 20000))
+        recs = S.gen_stream(int(rng.integers(1 << 30)), n, n_sets=int(rng.integers(1, 4)),
                             n_senders=int(rng.integers(1, 80)), jitter=int(rng.choice([0, 4, 8, 32, 200])), mode=mode)
         want, _ = O.encode(recs, 131072)
         if c.decode_stream(want) != O.decode(want):
@@ -213,6 +215,62 @@ def test_decode_tiers_vs_oracle(tier, monkeypatch):
             bad.append((t, mode, "records"))
     assert not bad, bad[:5]
     c.close()
+
+
+def _moved(n, rng, moves, reach):
+    """0..n-1 with `moves` elements taken out and put back up to `reach` places away."""
+    order = list(range(n))
+    for _ in range(moves):
+        i = int(rng.integers(0, n))
+        j = int(np.clip(i + rng.integers(-reach, reach + 1), 0, n - 1))
+        order.insert(j, order.pop(i))
+    return order
+
+
+@pytest.mark.parametrize("shape", ["dense_near", "dense_far", "sparse_far", "boundary_far", "blocks"])
+def test_decode_pair_segments_vs_oracle(shape):
+    """Tables whose pair lists span several segments of the permutation rebuild: dense short
+    moves (every segment checks out), moves that reach further than a segment replays or than
+    its window holds (the unit falls to the whole-unit tiers), a few long moves right where a
+    segment starts, and closed blocks of unequal density."""
+    rng = np.random.default_rng(len(shape) * 977 + 5)
+    c = ctx(131072)
+    bad = []
+    for t in range(4):
+        n = int(rng.integers(6000, 16000))
+        if shape == "dense_near":
+            order = _moved(n, rng, n, 12)
+        elif shape == "dense_far":
+            order = _moved(n, rng, n // 2, 150)
+        elif shape == "sparse_far":
+            order = _moved(n, rng, n // 2, 6)
+            for _ in range(8):
+                i = int(rng.integers(0, n))
+                order.insert(int(np.clip(i + rng.integers(-900, 900), 0, n - 1)), order.pop(i))
+        elif shape == "boundary_far":
+            order = _moved(n, rng, n, 10)
+            want_ids, _ = O.cdc_pairs(np.array(order, np.int32))
+            for s in range(1, len(want_ids) // 1024 + 1):  # disturb the list around every 1024th pair's id
+                x = int(want_ids[min(s * 1024, len(want_ids) - 1)])
+                for dx in (-70, -33, 5, 40):
+                    i = order.index(int(np.clip(x + dx, 0, n - 1)))
+                    order.insert(int(np.clip(i + rng.integers(-60, 60), 0, n - 1)), order.pop(i))
+        else:
+            order, base = [], 0
+            while base < n:
+                L = int(rng.choice([1, 5, 40, 300, 2500]))
+                blk = _moved(L, rng, int(L * rng.choice([0.0, 0.3, 1.5])), int(rng.choice([3, 20, 90])))
+                order += [base + v for v in blk]
+                base += L
+        recs = S.permutation_stream(order, src=4)
+        want, _ = O.encode(recs, 131072)
+        if c.decode_stream(want) != O.decode(want):
+            bad.append((shape, t, len(order), "tables"))
+            continue
+        keys = O.sorted_keys(recs, 131072)
+        if not np.array_equal(c.reconstruct_stream(want, keys), O.reconstruct(want, keys)):
+            bad.append((shape, t, len(order), "records"))
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("tier", [0, 1])
