@@ -504,6 +504,8 @@ def main():
               f"kernels sum {tot / 1e3:.3f}s; job wall {job_wall:.1f}s", file=sys.stderr)
         print(f"  chain tiers of the last encode of lane 0 (segments: all, past 16 leaves, past 64): "
               f"{lanes[0].ctx.chain_tiers()}", file=sys.stderr)
+        print(f"  rebuild tiers of the lanes' last decodes (tables: all, whole-table groups, window, list; segments: all, "
+              f"rerun, given up): {[ln.ctx.decode_tiers() for ln in lanes]}", file=sys.stderr)
         for note in ver["notes"][:20]:
             print("  verify:", note, file=sys.stderr)
 

@@ -323,6 +323,15 @@ int cdcx_chain_stats(cdcx_ctx* ctx, int64_t* out, int n);
  * out[2] segments that outgrew 64 slots (lane kernel, global-memory leaf list). */
 int cdcx_chain_tiers(cdcx_ctx* ctx, int64_t* out);
 
+/* Tables that entered each tier of the permutation rebuild (cdc_prepare_decode_indices,
+ * rempi_encoder_cdc.cpp:1301-1386) in the last decode: out[0] all tables (pair segments),
+ * out[1] tables with a segment that did not finish or did not check out (whole table in a
+ * 16-lane group), out[2] tables that left that one (256-slot window), out[3] tables replayed
+ * on the sequential list; out[4] the pair segments of the first tier, out[5] segment reruns
+ * (a segment whose replayed start differed from its predecessor's final state runs again from
+ * that state), out[6] segments that did not finish or still differed and sent their table on. */
+int cdcx_decode_tiers(cdcx_ctx* ctx, int64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -108,6 +108,7 @@ _SIGNATURES = {
     "cdcx_reset_kernel_times": ([_vp], ctypes.c_int),
     "cdcx_chain_stats": ([_vp, _i64p, ctypes.c_int], ctypes.c_int),
     "cdcx_chain_tiers": ([_vp, _i64p], ctypes.c_int),
+    "cdcx_decode_tiers": ([_vp, _i64p], ctypes.c_int),
 }
 
 _lib = None
@@ -393,6 +394,14 @@ class Context:
         """Segments entering each chain tier (16-lane, 64-lane, lane kernel) in the last encode."""
         out = np.zeros(3, dtype=np.int64)
         self._check(lib().cdcx_chain_tiers(self._c, _ptr(out, ctypes.c_int64)), "chain_tiers")
+        return [int(x) for x in out]
+
+    def decode_tiers(self):
+        """Tables entering each permutation-rebuild tier in the last decode (pair segments, whole
+        table in a 16-lane group, 256-slot window, sequential list), then the number of segments,
+        of segment reruns and of segments that sent their table to the next tier."""
+        out = np.zeros(7, dtype=np.int64)
+        self._check(lib().cdcx_decode_tiers(self._c, _ptr(out, ctypes.c_int64)), "decode_tiers")
         return [int(x) for x in out]
 
     def chain_stats(self):

@@ -221,6 +221,7 @@ struct cdcx_ctx {
   hipEvent_t gate_ev[kGateKinds][4] = {};
   int gate_next[kGateKinds] = {};
   int64_t chain_tier_counts[3] = {0, 0, 0};  // segments entering each tier in the last encode
+  int64_t dec_tier_counts[7] = {0, 0, 0, 0, 0, 0, 0};  // tables entering each rebuild tier in the last decode; segments
 
   template <class T>
   T* buf(const std::string& name, size_t count) {
@@ -864,19 +865,37 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   // sequential list.
   const int64_t nsegs = tot.segs;
   int32_t* d_cinv = c->buf<int32_t>(kAliasCinv, ko);
-  int32_t* d_nfail = c->buf<int32_t>("d_nfail", 4);
-  HIPCHK(hipMemsetAsync(d_nfail, 0, 16, s));
+  int32_t* d_nfail = c->buf<int32_t>("d_nfail", 8);  // units leaving tiers 0..2, -, segments not finished / not checking out
+  HIPCHK(hipMemsetAsync(d_nfail, 0, 32, s));
   DSeg* d_segs = c->buf<DSeg>("d_segs", nsegs);
   int64_t* d_pcar = c->buf<int64_t>("d_pcar", 4 * nsegs);
   int32_t* d_dump_t = c->buf<int32_t>("d_dump_t", (size_t)nsegs * kSegWin);
   int32_t* d_dump_w = c->buf<int32_t>("d_dump_w", (size_t)nsegs * kSegWin);
-  c->launch(K_DEC_PAIRS, k_dec_pair_scan, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, 1 | (pairs ? 4 : 0), d_segs,
+  c->launch(K_DEC_PAIRS, k_dec_pair_scan, dim3(NU), dim3(64), s, (const DUnit*)d_units, d_in, 1 | (pairs ? 4 : 0), d_segs,
             d_pcar, d_idd, d_dld);
-  c->launch_gated(1, NU >= 4096, K_DEC_SEG, k_dec_perm_seg<true>, dim3(blocks(nsegs, 4)), dim3(64), s, d_units,
+  c->launch_gated(1, NU >= 4096, K_DEC_SEG, k_dec_perm_seg<1>, dim3(blocks(nsegs, 4)), dim3(64), s, d_units,
                   (const int32_t*)nullptr, (const DSeg*)d_segs, nsegs, 0, d_in, (const int64_t*)d_pcar, d_perm, d_cinv,
                   d_dump_t, d_dump_w, d_nfail);
-  c->launch(K_DEC_CHECK, k_dec_perm_check, dim3(blocks(nsegs, 8)), dim3(256), s, d_units, (const DSeg*)d_segs, nsegs,
-            (const int32_t*)d_dump_t, (const int32_t*)d_dump_w, d_nfail);
+  // Segments that did not start from their predecessor's final state (a few in 10^5 on the bench
+  // traces) run again from that state, twice if the first rerun changed what a neighbour started
+  // from; what still differs then sends its unit to the next tier.
+  constexpr int32_t kRedoCap = 1024, kRedoRounds = 2;
+  int32_t* d_redo = c->buf<int32_t>("d_redo", (size_t)kRedoRounds * (kRedoCap + 1));
+  int32_t* d_redone = c->buf<int32_t>("d_redone", NU);
+  HIPCHK(hipMemsetAsync(d_redo, 0, sizeof(int32_t) * kRedoRounds * (kRedoCap + 1), s));
+  HIPCHK(hipMemsetAsync(d_redone, 0, sizeof(int32_t) * (size_t)NU, s));
+  if (nsegs > NU)
+    for (int32_t round = 0; round <= kRedoRounds; round++) {
+      int32_t* list = round < kRedoRounds ? d_redo + round * (kRedoCap + 1) : nullptr;
+      c->launch(K_DEC_CHECK, k_dec_perm_check, dim3(blocks(nsegs, 8)), dim3(256), s, d_units, (const DSeg*)d_segs, nsegs,
+                (const int32_t*)d_dump_t, (const int32_t*)d_dump_w, list, kRedoCap, d_redone, d_nfail);
+      if (list)
+        c->launch(K_DEC_SEG, k_dec_perm_seg<2>, dim3(kRedoCap / 4), dim3(64), s, d_units, (const int32_t*)list,
+                  (const DSeg*)d_segs, (int64_t)kRedoCap, 0, d_in, (const int64_t*)d_pcar, d_perm, d_cinv, d_dump_t,
+                  d_dump_w, d_nfail);
+    }
+  c->launch(K_DEC_CHECK, k_dec_perm_inv, dim3(NU), dim3(256), s, (const DUnit*)d_units, (const int32_t*)d_redone,
+            (const int32_t*)d_cinv, d_perm);
   // The record tiles are listed while the rebuild runs; the reconstruction itself is launched
   // before the wait for the failure count when no unit can have failed into a later tier.
   int4* d_rt = nullptr;
@@ -892,25 +911,34 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   int32_t nf = NU;
   {
     Mail m(c, s, 64);
-    const size_t o_err = m.add(d_err, 4), o = m.add(d_nfail, 4);
+    const size_t o_err = m.add(d_err, 4), o = m.add(d_nfail, 32);
     const uint8_t* h = m.wait();
     raise_device_error(*reinterpret_cast<const uint32_t*>(h + o_err));
-    if (c->dec_tier <= 0) nf = *reinterpret_cast<const int32_t*>(h + o);
+    const int32_t* cnt = reinterpret_cast<const int32_t*>(h + o);
+    if (c->dec_tier <= 0) nf = cnt[0];
+    c->dec_tier_counts[5] = cnt[5];
+    c->dec_tier_counts[6] = cnt[4] + cnt[6];
   }
+  c->dec_tier_counts[0] = NU;
+  c->dec_tier_counts[1] = nf;
+  c->dec_tier_counts[2] = c->dec_tier_counts[3] = 0;
+  c->dec_tier_counts[4] = nsegs;
   if (nf > 0) {
     if (!pairs)  // the later tiers read the decoded pair arrays
-      c->launch(K_DEC_PAIRS, k_dec_pair_scan, dim3(NU), dim3(256), s, (const DUnit*)d_units, d_in, 2, (DSeg*)nullptr,
+      c->launch(K_DEC_PAIRS, k_dec_pair_scan, dim3(NU), dim3(64), s, (const DUnit*)d_units, d_in, 2, (DSeg*)nullptr,
                 (int64_t*)nullptr, d_idd, d_dld);
     int32_t* d_order = c->buf<int32_t>("d_perm_order", NU);
     c->launch(K_LISTS, k_dec_order, dim3(blocks(NU, 256)), dim3(256), s, (const DUnit*)d_units, NU, d_order);
-    c->launch(K_DEC_WIN1, k_dec_perm_seg<false>, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order,
+    c->launch(K_DEC_WIN1, k_dec_perm_seg<0>, dim3(blocks(NU, 4)), dim3(64), s, d_units, (const int32_t*)d_order,
               (const DSeg*)nullptr, (int64_t)NU, 1, d_in, (const int64_t*)nullptr, d_perm, d_cinv, (int32_t*)nullptr,
               (int32_t*)nullptr, d_nfail + 1);
     const int32_t nf1 = c->dec_tier > 1 ? NU : c->download(d_nfail + 1, 1, s)[0];
+    c->dec_tier_counts[2] = nf1;
     if (nf1 > 0) {
       c->launch(K_DEC_WIN4, k_dec_perm_window<4>, dim3(NU), dim3(64), s, d_units, NU, 2, (const uint64_t*)d_idd,
                 (const uint64_t*)d_dld, d_perm, d_nfail + 2);
       const int32_t nf2 = c->dec_tier > 2 ? NU : c->download(d_nfail + 2, 1, s)[0];
+      c->dec_tier_counts[3] = nf2;
       if (nf2 > 0) {
         int32_t* d_nx = c->buf<int32_t>("d_nx", wb);  // the sequential list only exists when needed
         int32_t* d_pv = c->buf<int32_t>("d_pv", wb);
@@ -1553,9 +1581,9 @@ int cdcx_decode_chunk_perm_static(cdcx_ctx* c, const uint8_t* d_payload, size_t 
   const int64_t cap = (int64_t)std::min<size_t>(perm_capacity, (size_t)kStaticMaxRows);
   hipLaunchKernelGGL(k_dec_chunk_units, dim3(1), dim3(64), 0, s, d_payload, (int64_t)len, kStaticMaxUnits, kStaticMaxRows, cap,
                      hdr, order, units);
-  hipLaunchKernelGGL(k_dec_pair_scan, dim3(kStaticMaxUnits), dim3(256), 0, s, (const DUnit*)units, d_payload, 4, (DSeg*)nullptr,
+  hipLaunchKernelGGL(k_dec_pair_scan, dim3(kStaticMaxUnits), dim3(64), 0, s, (const DUnit*)units, d_payload, 4, (DSeg*)nullptr,
                      (int64_t*)nullptr, idd, dld);
-  hipLaunchKernelGGL(k_dec_perm_seg<false>, dim3(kStaticMaxUnits / 4), dim3(64), 0, s, units, (const int32_t*)order,
+  hipLaunchKernelGGL(k_dec_perm_seg<0>, dim3(kStaticMaxUnits / 4), dim3(64), 0, s, units, (const int32_t*)order,
                      (const DSeg*)nullptr, (int64_t)kStaticMaxUnits, 1, d_payload, (const int64_t*)nullptr, d_perm, cinv,
                      (int32_t*)nullptr, (int32_t*)nullptr, hdr + 2);
   hipLaunchKernelGGL(k_dec_perm_window<4>, dim3(kStaticMaxUnits), dim3(64), 0, s, units, kStaticMaxUnits, 2,
@@ -1971,6 +1999,12 @@ int cdcx_kernel_times(cdcx_ctx* c, double* ms, int64_t* launches, int n) {
 int cdcx_chain_tiers(cdcx_ctx* c, int64_t* out) {
   if (!c || !out) return CDCX_ERR_ARG;
   for (int k = 0; k < 3; k++) out[k] = c->chain_tier_counts[k];
+  return CDCX_OK;
+}
+
+int cdcx_decode_tiers(cdcx_ctx* c, int64_t* out) {
+  if (!c || !out) return CDCX_ERR_ARG;
+  for (int k = 0; k < 7; k++) out[k] = c->dec_tier_counts[k];
   return CDCX_OK;
 }
 

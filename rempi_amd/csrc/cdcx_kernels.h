@@ -100,10 +100,12 @@ __global__ void k_dec_sections(const DUnit*, const uint8_t*, uint64_t*, uint64_t
 __global__ void k_dec_perm_lane(const DUnit*, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*, int32_t*,
                                 uint32_t*);
 __global__ void k_dec_pair_scan(const DUnit*, const uint8_t*, int32_t, DSeg*, int64_t*, uint64_t*, uint64_t*);
-template <bool SEG>
+template <int MODE>
 __global__ void k_dec_perm_seg(DUnit*, const int32_t*, const DSeg*, int64_t, int32_t, const uint8_t*, const int64_t*,
                                int32_t*, int32_t*, int32_t*, int32_t*, int32_t*);
-__global__ void k_dec_perm_check(DUnit*, const DSeg*, int64_t, const int32_t*, const int32_t*, int32_t*);
+__global__ void k_dec_perm_check(DUnit*, const DSeg*, int64_t, const int32_t*, const int32_t*, int32_t*, int32_t, int32_t*,
+                                 int32_t*);
+__global__ void k_dec_perm_inv(const DUnit*, const int32_t*, const int32_t*, int32_t*);
 __global__ void k_dec_cinv(const DUnit*, const int32_t*, int32_t*);
 template <int K>
 __global__ void k_dec_perm_window(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);

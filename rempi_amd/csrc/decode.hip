@@ -461,69 +461,52 @@ template __global__ void k_dec_perm_window<4>(DUnit*, int32_t, int32_t, const ui
 //   mode & 2: the decoded pair arrays of the units that left the first tier (fb != 0);
 //   mode & 4: the decoded pair arrays of every unit (table dumps).
 namespace {
-// exclusive prefix sums of two words over the 256 threads (wsum: [4][4] words of LDS)
-__device__ __forceinline__ void block_scan2(uint64_t a, uint64_t b, uint64_t (*wsum)[4], uint64_t* ea, uint64_t* eb,
-                                            uint64_t* ta, uint64_t* tb) {
-  const int w = threadIdx.x >> 6;
-  const uint64_t ia = wave_inclusive_scan(a, OpAdd()), ib = wave_inclusive_scan(b, OpAdd());
-  __syncthreads();  // (the previous call's readers are done)
-  if (lane_id() == kWave - 1) {
-    wsum[w][0] = ia;
-    wsum[w][1] = ib;
-  }
-  __syncthreads();
-  uint64_t pa = 0, pb = 0, sa = 0, sb = 0;
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const uint64_t va = wsum[q][0], vb = wsum[q][1];
-    if (q < w) {
-      pa += va;
-      pb += vb;
-    }
-    sa += va;
-    sb += vb;
-  }
-  *ea = pa + ia - a;
-  *eb = pb + ib - b;
-  *ta = sa;
-  *tb = sb;
-}
 __device__ __forceinline__ int32_t seg_floor(int32_t min_id) { return max(0, min_id - kSegDelta) & ~15; }
 }  // namespace
 
-__global__ void __launch_bounds__(256) k_dec_pair_scan(const DUnit* __restrict__ units, const uint8_t* __restrict__ in,
-                                                       int32_t mode, DSeg* __restrict__ segs, int64_t* __restrict__ pcar,
-                                                       uint64_t* __restrict__ idd, uint64_t* __restrict__ dld) {
+// One wave per unit and no workgroup barrier: a unit's pairs are one chain of prefix sums, 256
+// pairs per round (four per lane, the next round's words already in flight), and a wave on its
+// own is not held up by the other waves of a workgroup when the GPU is busy with other streams.
+__global__ void __launch_bounds__(64) k_dec_pair_scan(const DUnit* __restrict__ units, const uint8_t* __restrict__ in,
+                                                      int32_t mode, DSeg* __restrict__ segs, int64_t* __restrict__ pcar,
+                                                      uint64_t* __restrict__ idd, uint64_t* __restrict__ dld) {
   __shared__ int32_t bmin[kSegMaxP / kSegWarm + 1];  // smallest id of every kSegWarm pairs, then suffix minima
-  __shared__ uint64_t wsum[4][4];
   const int32_t ui = blockIdx.x;
   const DUnit u = units[ui];
-  const int32_t P = u.P, tid = threadIdx.x;
+  const int32_t P = u.P, l = threadIdx.x;
   const bool lists = (mode & 1) && u.nseg > 1;  // (more than one segment: P <= kSegMaxP)
   const bool store = (mode & 4) || ((mode & 2) && u.fb != 0);
-  if ((mode & 1) && u.nseg <= 1 && tid == 0)
-    segs[u.seg0] = DSeg{ui, 0, 0, P, 0, kSegNoCap, 0, 0};
+  if ((mode & 1) && u.nseg <= 1 && l == 0) segs[u.seg0] = DSeg{ui, 0, 0, P, 0, kSegNoCap, 0, 0};
   if (!lists && !store) return;
   const int32_t* yid = reinterpret_cast<const int32_t*>(in + u.pair_off);
   const int32_t* ydl = yid + P;
-  uint64_t czi = 0, cxi = 0, czd = 0, cxd = 0;  // z, x before the tile's first pair
-  for (int32_t t0 = 0; t0 < P; t0 += 1024) {
-    const int32_t k = t0 + 4 * tid;
+  uint64_t czi = 0, cxi = 0, czd = 0, cxd = 0;  // z, x before the round's first pair
+  int32_t wi[4], wd[4];
+  auto load = [&](int32_t k) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      wi[q] = (k + q < P) ? yid[k + q] : 0;
+      wd[q] = (k + q < P) ? ydl[k + q] : 0;
+    }
+  };
+  load(4 * l);
+  for (int32_t t0 = 0; t0 < P; t0 += 256) {
+    const int32_t k = t0 + 4 * l;
     uint64_t zi[4], zd[4], s2i = 0, s2d = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const bool inb = k + q < P;
-      const uint64_t yi = inb ? sext(yid[k + q]) : 0, yd = inb ? sext(ydl[k + q]) : 0;
-      zi[q] = (q ? zi[q - 1] : 0) + yi;
-      zd[q] = (q ? zd[q - 1] : 0) + yd;
+      zi[q] = (q ? zi[q - 1] : 0) + sext(wi[q]);
+      zd[q] = (q ? zd[q - 1] : 0) + sext(wd[q]);
       s2i += zi[q];
       s2d += zd[q];
     }
-    uint64_t zoi, zod, tzi, tzd, xoi, xod, txi, txd;
-    block_scan2(zi[3], zd[3], wsum, &zoi, &zod, &tzi, &tzd);
-    block_scan2(4 * zoi + s2i, 4 * zod + s2d, wsum, &xoi, &xod, &txi, &txd);
+    load(k + 256);  // (in flight during the scans)
+    const uint64_t zni = wave_inclusive_scan(zi[3], OpAdd()), znd = wave_inclusive_scan(zd[3], OpAdd());
+    const uint64_t zoi = zni - zi[3], zod = znd - zd[3];
+    const uint64_t ai = 4 * zoi + s2i, ad = 4 * zod + s2d;
+    const uint64_t xni = wave_inclusive_scan(ai, OpAdd()), xnd = wave_inclusive_scan(ad, OpAdd());
     const uint64_t z0i = czi + zoi, z0d = czd + zod;
-    uint64_t xi = cxi + 4 * czi * (uint64_t)tid + xoi, xd = cxd + 4 * czd * (uint64_t)tid + xod;
+    uint64_t xi = cxi + 4 * czi * (uint64_t)l + (xni - ai), xd = cxd + 4 * czd * (uint64_t)l + (xnd - ad);
     if (lists && (k & (kSegWarm - 1)) == 0 && ((k / kSegWarm) & 7) == 7) {  // k = s * kSegPairs - kSegWarm
       const int32_t sg = (k / kSegWarm + 1) >> 3;
       if (sg < u.nseg) {
@@ -550,28 +533,24 @@ __global__ void __launch_bounds__(256) k_dec_pair_scan(const DUnit* __restrict__
     if (lists) {
 #pragma unroll
       for (int dlt = 16; dlt >= 1; dlt >>= 1) mn = min(mn, __shfl_xor(mn, dlt, 64));
-      if ((tid & 31) == 0) bmin[(t0 >> 7) + (tid >> 5)] = mn;
+      if ((l & 31) == 0) bmin[(t0 >> 7) + (l >> 5)] = mn;
     }
-    cxi += 1024 * czi + txi;
-    cxd += 1024 * czd + txd;
-    czi += tzi;
-    czd += tzd;
+    cxi += 256 * czi + __shfl(xni, kWave - 1, kWave);
+    cxd += 256 * czd + __shfl(xnd, kWave - 1, kWave);
+    czi += __shfl(zni, kWave - 1, kWave);
+    czd += __shfl(znd, kWave - 1, kWave);
   }
   if (!lists) return;
-  __syncthreads();
   const int32_t nb = (P + kSegWarm - 1) / kSegWarm;
-  if (tid < kWave) {  // suffix minima, 64 entries at a time from the top
-    int32_t carry = INT32_MAX;
-    for (int32_t hi = nb; hi > 0; hi -= kWave) {
-      const int32_t idx = hi - 1 - tid;
-      int32_t v = idx >= 0 ? bmin[idx] : INT32_MAX;
-      v = min(wave_inclusive_scan(v, OpMin()), carry);
-      if (idx >= 0) bmin[idx] = v;
-      carry = __shfl(v, kWave - 1, kWave);
-    }
+  int32_t carry = INT32_MAX;  // suffix minima, 64 entries at a time from the top
+  for (int32_t hi = nb; hi > 0; hi -= kWave) {
+    const int32_t idx = hi - 1 - l;
+    int32_t v = idx >= 0 ? bmin[idx] : INT32_MAX;
+    v = min(wave_inclusive_scan(v, OpMin()), carry);
+    if (idx >= 0) bmin[idx] = v;
+    carry = __shfl(v, kWave - 1, kWave);
   }
-  __syncthreads();
-  for (int32_t sg = tid; sg < u.nseg; sg += 256) {
+  for (int32_t sg = l; sg < u.nseg; sg += kWave) {
     const int32_t ka = sg * kSegPairs;
     DSeg d;
     d.unit = ui;
@@ -651,7 +630,7 @@ __device__ __forceinline__ int32_t row_bcast(int32_t v) {
 }
 }  // namespace
 
-template <bool SEG>
+template <int MODE>  // 0: whole units (`order`), 1: all segments, 2: the segments listed in `order` again, from dumpT
 __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, const int32_t* __restrict__ order,
                                                      const DSeg* __restrict__ segs, int64_t n_items, int32_t want_fb,
                                                      const uint8_t* __restrict__ in, const int64_t* __restrict__ pcar,
@@ -664,10 +643,19 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
   const int g = threadIdx.x >> 4, j = threadIdx.x & 15;
   int32_t* win = win_all[g];
   int2* emap = emap_all[g];
-  const int64_t gi = (int64_t)blockIdx.x * 4 + g;
+  constexpr bool SEG = MODE != 0, REDO = MODE == 2;
+  int64_t gi = (int64_t)blockIdx.x * 4 + g;
   int32_t ui = -1;
   DSeg sd{-1, 0, 0, 0, 0, kSegNoCap, 0, 0};
-  if (gi < n_items) {
+  if (REDO) {  // order[0]: entries listed (may exceed the list's n_items slots), order[1 + k]: segment
+    const int64_t k = gi;
+    gi = -1;
+    if (k < min((int64_t)order[0], n_items)) {
+      gi = order[1 + k];
+      sd = segs[gi];
+      ui = sd.unit;
+    }
+  } else if (gi < n_items) {
     if (SEG) {
       sd = segs[gi];
       ui = sd.unit;
@@ -832,16 +820,35 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
       lp(warm_t, kb + i0, ai, ad);
       ai = ld(yid, kb + i0 + 32);
       ad = ld(ydl, kb + i0 + 32);
-      steps(warm_t, kb + i0, 16);
+      if (!REDO) steps(warm_t, kb + i0, 16);
       lp(warm_t, kb + i0 + 16, bi, bd);
       bi = ld(yid, kb + i0 + 48);
       bd = ld(ydl, kb + i0 + 48);
-      steps(warm_t, kb + i0 + 16, 16);
+      if (!REDO) steps(warm_t, kb + i0 + 16, 16);
     }
-    // the window moves up to the first owned position; the state there goes to the check
-    while (__builtin_amdgcn_ballot_w64(wact && base < own)) slide(warm_t, wact && base < own);
-    if (wact)
-      for (int32_t q = j; q < W; q += 16) dumpW[gi * W + q] = win[(base + q) & WM];
+    if (REDO) {
+      // again, from the state the predecessor ended in (only the LP state came from the pairs
+      // before): that state is now also the one this segment is on record as having started from
+      if (wact) {
+        base = own;
+        for (int32_t q = j; q < kGMap; q += 16) emap[q] = make_int2(-1, -1);
+        for (int32_t q = j; q < W; q += 16) {
+          const int32_t v = dumpT[gi * W + q];
+          dumpW[gi * W + q] = v;
+          win[(own + q) & WM] = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int32_t q = j; q < W; q += 16) {
+          const int32_t v = win[(own + q) & WM];
+          emap[v & MM] = make_int2(v, own + q);
+        }
+      }
+    } else {
+      // the window moves up to the first owned position; the state there goes to the check
+      while (__builtin_amdgcn_ballot_w64(wact && base < own)) slide(warm_t, wact && base < own);
+      if (wact)
+        for (int32_t q = j; q < W; q += 16) dumpW[gi * W + q] = win[(base + q) & WM];
+    }
     if (!wact) {  // (a group without a replay went through it with zero words: nothing to carry over)
       czi = cxi = czd = cxd = 0;
     }
@@ -864,6 +871,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
   const bool fail = failv != 0;
   if (sim && fail && j == 0) {
     if (atomicCAS(&units[ui].fb, want_fb, want_fb + 1) == want_fb) atomicAdd(nfail, 1);
+    if (SEG) atomicAdd(nfail + 4, 1);  // (diagnostics: segment runs that did not finish)
   }
   if (!fail) {
     const int32_t lim = min(M, cap);  // the positions below are this group's to write
@@ -883,17 +891,27 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
   }
 }
 
-template __global__ void k_dec_perm_seg<true>(DUnit*, const int32_t*, const DSeg*, int64_t, int32_t, const uint8_t*,
-                                              const int64_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*);
-template __global__ void k_dec_perm_seg<false>(DUnit*, const int32_t*, const DSeg*, int64_t, int32_t, const uint8_t*,
-                                               const int64_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*);
+template __global__ void k_dec_perm_seg<0>(DUnit*, const int32_t*, const DSeg*, int64_t, int32_t, const uint8_t*,
+                                           const int64_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*);
+template __global__ void k_dec_perm_seg<1>(DUnit*, const int32_t*, const DSeg*, int64_t, int32_t, const uint8_t*,
+                                           const int64_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*);
+template __global__ void k_dec_perm_seg<2>(DUnit*, const int32_t*, const DSeg*, int64_t, int32_t, const uint8_t*,
+                                           const int64_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*);
 
 // The state a segment starts its own pairs from (dumpW) against the state its predecessor
 // ends in (dumpT), kSegWin list positions from the segment's first owned one; 32 lanes per
-// segment.  A difference sends the unit to the next tier.
+// segment.  A segment that differs is listed in `redo` (redo[0] counts, redo[1..cap] hold the
+// segments) and its unit marked in `redone`: k_dec_perm_seg<2> runs it again from dumpT, which
+// is the sequential replay's state if the segments before it check out -- and the next check
+// looks at all of them again.  The last check (`redo` null), or a full list, sends the unit to
+// the next tier instead.  (A redone segment's earlier run may have written perm entries of
+// elements that are not in its positions after all: k_dec_perm_inv rewrites perm of the marked
+// units from cinv, which is indexed by position and so holds each segment's last run only.)
 __global__ void __launch_bounds__(256) k_dec_perm_check(DUnit* __restrict__ units, const DSeg* __restrict__ segs,
                                                         int64_t nsegs, const int32_t* __restrict__ dumpT,
-                                                        const int32_t* __restrict__ dumpW, int32_t* __restrict__ nfail) {
+                                                        const int32_t* __restrict__ dumpW, int32_t* __restrict__ redo,
+                                                        int32_t redo_cap, int32_t* __restrict__ redone,
+                                                        int32_t* __restrict__ nfail) {
   static_assert(kSegWin == 128, "32 lanes x int4");
   const int64_t gi = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
   const int l = threadIdx.x & 31;
@@ -909,8 +927,25 @@ __global__ void __launch_bounds__(256) k_dec_perm_check(DUnit* __restrict__ unit
   }
   const uint64_t m = __builtin_amdgcn_ballot_w64(diff);
   if (l == 0 && ui >= 0 && ((m >> (threadIdx.x & 32)) & 0xffffffffull)) {
-    if (atomicCAS(&units[ui].fb, 0, 1) == 0) atomicAdd(nfail, 1);
+    int32_t slot = redo_cap;
+    if (redo) slot = atomicAdd(redo, 1);
+    if (slot < redo_cap) {
+      redo[1 + slot] = (int32_t)gi;
+      redone[ui] = 1;
+      atomicAdd(nfail + 5, 1);  // (diagnostics: segments run again)
+    } else {
+      if (atomicCAS(&units[ui].fb, 0, 1) == 0) atomicAdd(nfail, 1);
+      atomicAdd(nfail + 6, 1);  // (diagnostics: segments that sent their unit on)
+    }
   }
+}
+
+__global__ void __launch_bounds__(256) k_dec_perm_inv(const DUnit* __restrict__ units, const int32_t* __restrict__ redone,
+                                                      const int32_t* __restrict__ cinv, int32_t* __restrict__ perm) {
+  if (!redone[blockIdx.x]) return;
+  const DUnit u = units[blockIdx.x];
+  if (u.fb != 0) return;  // (a later tier rewrites both arrays)
+  for (int32_t i = threadIdx.x; i < u.M; i += 256) perm[u.key_off + cinv[u.key_off + i]] = i;
 }
 
 // Rows whose permutation came from the fallback kernels: c = perm^-1.

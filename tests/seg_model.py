@@ -88,12 +88,17 @@ class Group:
         return True
 
 
-def run_segment(ids, dl, M, seg, first):
-    """-> (ok, written positions, state it started its own pairs from, state it ends in)"""
+def run_segment(ids, dl, M, seg, first, from_state=None):
+    """-> (ok, written positions, state it started its own pairs from, state it ends in);
+    from_state: run again from this state at `own` instead of the replay (k_dec_perm_seg<2>)"""
     ka, ke, own, cap, base0 = seg
     g = Group(M, base0)
     start = None
-    if not first:
+    if from_state is not None:
+        g.base = own
+        g.win = list(from_state)
+        start = list(from_state)
+    elif not first:
         for k in range(ka - WARM, ka):
             g.step(int(ids[k]), int(dl[k]), True, own)
         while g.base < own:
@@ -115,15 +120,22 @@ def run_segment(ids, dl, M, seg, first):
     return True, g.out, start, end
 
 
-def rebuild(ids, dl, M):
-    """The tier on one unit: perm (list) if every segment finishes and checks out, else None
-    (the unit goes to the whole-unit tiers)."""
+def rebuild(ids, dl, M, stats=None):
+    """The tier on one unit: perm (list) if every segment finishes and starts from the state its
+    predecessor ended in -- after running again from that state where its replay gave another
+    (the device gives up after two rounds of such reruns; here every segment gets one, in order,
+    which is where those rounds end up when they suffice) -- else None (the unit goes to the
+    whole-unit tiers).  perm is read off cinv, as k_dec_perm_inv does after reruns."""
     segs = layout(ids)
     cinv = {}
     prev_end = None
     for s, seg in enumerate(segs):
         ok, out, start, end = run_segment(ids, dl, M, seg, s == 0)
-        if not ok or (s > 0 and start != prev_end):
+        if ok and s > 0 and start != prev_end:
+            if stats is not None:
+                stats["reruns"] = stats.get("reruns", 0) + 1
+            ok, out, start, end = run_segment(ids, dl, M, seg, False, from_state=prev_end)
+        if not ok:
             return None
         cinv.update(out)
         prev_end = end

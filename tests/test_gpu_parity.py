@@ -135,6 +135,8 @@ def test_batch_encode_decode_vs_oracle(batch):
     keys = cdcx.d2h(d_keys, n_keys * 8, np.int32).reshape(-1, 2)
     np.testing.assert_array_equal(keys, np.concatenate([O.sorted_keys(h, 131072) for h in host]))
     d_recs, n_recs, d_perm = c.decode_batch_device(d_out, off, ln, d_keys, n_keys)
+    tiers = c.decode_tiers()
+    assert tiers[1] == 0 and tiers[4] > tiers[0], tiers  # the bench workload stays in the segment tier
     recs = cdcx.d2h(d_recs, n_recs * 32, np.int32).reshape(-1, 8)
     want = np.concatenate([S.expected_table_streams(h, 131072) for h in host])
     np.testing.assert_array_equal(recs, want)
@@ -217,6 +219,22 @@ def test_decode_tiers_vs_oracle(tier, monkeypatch):
     c.close()
 
 
+def test_decode_segment_rerun_vs_oracle():
+    """Rank 317 of the bench workload at 400 K events has a pair segment (one in about 10^5 has)
+    whose replay of the 128 pairs before it does not give the state its predecessor ends in: the
+    state check finds it, the segment runs again from the predecessor's state, and the tables
+    are the reference's without the table leaving the first tier."""
+    p = rempi_amd.default_gen_params(world_size=1024, events_per_rank=400_000)
+    recs = rempi_amd.generate_host(p, 317)
+    want, _ = O.encode(recs, 131072)
+    c = ctx(131072)
+    assert c.decode_stream(want) == O.decode(want)
+    tiers = c.decode_tiers()
+    assert tiers[5] >= 1 and tiers[1] == 0 and tiers[6] == 0, tiers
+    keys = O.sorted_keys(recs, 131072)
+    np.testing.assert_array_equal(c.reconstruct_stream(want, keys), O.reconstruct(want, keys))
+
+
 def _moved(n, rng, moves, reach):
     """0..n-1 with `moves` elements taken out and put back up to `reach` places away."""
     order = list(range(n))
@@ -267,6 +285,11 @@ def test_decode_pair_segments_vs_oracle(shape):
         if c.decode_stream(want) != O.decode(want):
             bad.append((shape, t, len(order), "tables"))
             continue
+        tiers = c.decode_tiers()
+        if shape == "dense_near":
+            assert tiers[4] > tiers[0] and tiers[1] == 0, tiers  # several segments, all checked out
+        if shape == "dense_far":
+            assert tiers[4] > tiers[0] and tiers[1] > 0, tiers  # moves past the window: the table left the first tier
         keys = O.sorted_keys(recs, 131072)
         if not np.array_equal(c.reconstruct_stream(want, keys), O.reconstruct(want, keys)):
             bad.append((shape, t, len(order), "records"))
