@@ -509,8 +509,9 @@ def main():
         for note in ver["notes"][:20]:
             print("  verify:", note, file=sys.stderr)
 
+    # (after the last collective: with several GPU processes only rank 0 is still busy here)
     cpu = None
-    if args.cpu_baseline and rank == 0 and ws == 1:
+    if args.cpu_baseline and rank == 0:
         cpu = cpu_baseline(args)
 
     if rank == 0:

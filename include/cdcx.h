@@ -211,8 +211,10 @@ int cdcx_decode_batch_device(cdcx_ctx* ctx, int32_t n_ranks, const uint8_t* d_in
                              const int32_t** d_perm, void* stream);
 
 /* The one entry point that allocates nothing.  It has no counterpart in the reference; it is
- * for callers that cannot allocate device memory: code under HIP graph capture, tight replay
- * loops, harnesses that forbid hipMalloc.  A variant of cdcx_decode_batch_device (tables
+ * for callers that cannot allocate device memory: tight replay loops, harnesses that forbid
+ * hipMalloc.  (Not for a stream under HIP graph capture: the call waits for the stream and
+ * copies its status words to the host, neither of which a capturing stream allows.)  A variant
+ * of cdcx_decode_batch_device (tables
  * only) for ONE chunk already in device memory: d_payload is the chunk payload (what follows
  * the size_t length in the file, plain CDC), and d_perm receives the
  * matched_events_permutated_indices (cdc_prepare_decode_indices, :1301-1386) of the chunk's
@@ -222,6 +224,8 @@ int cdcx_decode_batch_device(cdcx_ctx* ctx, int32_t n_ranks, const uint8_t* d_in
  * All scratch (unit table, pair rows, list links; 7 MiB) is a file-scope device array that
  * each GPU the library runs on holds until the process ends.  Limits: at most 256 tables and
  * sum(count + 1) <= 262144 per chunk (REMPI_MAX = 131072 chunks fit), else CDCX_ERR_LIMIT.
+ * d_payload must be 8-byte aligned and d_perm 4-byte aligned (CDCX_ERR_ARG otherwise, as for a
+ * REMPI_GZIP context: the payload must be plain CDC).
  * Calls no hipMalloc / hipFree; it does wait for the stream once, to read the status.
  * Every call on a GPU uses that GPU's one array: calls that overlap on one GPU (other
  * streams, other contexts or threads) race -- serialise them. */

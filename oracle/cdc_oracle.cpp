@@ -352,6 +352,11 @@ struct DecodedTable {
 // 0..M-1; for each pair, take `id` out, step `delay` nodes from its old successor and put
 // it back in front of that node.  perm[v] = final position of v.  The list is circular
 // with a sentinel (index M) as libstdc++'s std::list is.
+// 0 (default): a delay that walks more than once round the list is refused, as the device path
+// refuses it; 1: walk on through the sentinel however far, as std::advance on libstdc++'s
+// circular std::list does in the reference (oracle_set_reference_walk).
+static int g_reference_walk = 0;
+
 int decode_perm(const u64* ids, const u64* delays, int64_t P, int64_t M, int32_t* perm) {
   std::vector<int64_t> nx(M + 1), pv(M + 1);
   for (int64_t i = 0; i <= M; i++) {
@@ -365,7 +370,7 @@ int decode_perm(const u64* ids, const u64* delays, int64_t P, int64_t M, int32_t
     // The encoder never writes a delay that walks more than once round the list; the
     // reference would keep stepping through the std::list sentinel.  Treated as corrupt so
     // that damaged files cost O(M) per pair at most.
-    if (dl > M || dl < -M) return ORACLE_ERR_CORRUPT;
+    if (!g_reference_walk && (dl > M || dl < -M)) return ORACLE_ERR_CORRUPT;
     int64_t at = nx[id];
     nx[pv[id]] = nx[id];
     pv[nx[id]] = pv[id];
@@ -553,6 +558,8 @@ int oracle_cdc_pairs(const int32_t* c, int64_t M, int32_t* ids, int32_t* deltas,
   std::copy(d.begin(), d.end(), deltas);
   return ORACLE_OK;
 }
+
+void oracle_set_reference_walk(int on) { g_reference_walk = on != 0; }
 
 int oracle_decode_perm(const int64_t* ids, const int64_t* delays, int64_t P, int64_t M, int32_t* perm) {
   std::vector<u64> a(ids, ids + P), d(delays, delays + P);

@@ -45,7 +45,13 @@ int oracle_decode(const uint8_t* in, size_t len, uint8_t** out, size_t* out_len)
  * linear prediction.  ids/deltas must hold M entries; *P receives the pair count. */
 int oracle_cdc_pairs(const int32_t* c, int64_t M, int32_t* ids, int32_t* deltas, int64_t* P);
 
-/* cdc_prepare_decode_indices: pairs (already inverse-predicted) -> perm[M]. */
+/* cdc_prepare_decode_indices: pairs (already inverse-predicted) -> perm[M].
+ * One deliberate difference from the reference, shared with the device path: a delay that
+ * would walk more than once round the list (|delay| > M, never written by the encoder) is
+ * ORACLE_ERR_CORRUPT.  The reference's std::advance keeps stepping through the std::list
+ * sentinel; oracle_set_reference_walk(1) restores exactly that (for the test that pins it
+ * against the reference decoder), oracle_set_reference_walk(0) the default. */
+void oracle_set_reference_walk(int on);
 int oracle_decode_perm(const int64_t* ids, const int64_t* delays, int64_t P, int64_t M, int32_t* perm);
 
 /* Iteration order of a libstdc++ std::unordered_map<size_t,size_t> after inserting the

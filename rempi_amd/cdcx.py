@@ -122,6 +122,8 @@ def lib() -> ctypes.CDLL:
             raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
         L = ctypes.CDLL(LIB_PATH)
         for name, (args, res) in _SIGNATURES.items():
+            if "CDCX_LIB" in os.environ and not hasattr(L, name):
+                continue  # (an older build in an A/B run: its diagnostics calls then fail when used)
             f = getattr(L, name)
             f.argtypes = args
             f.restype = res

@@ -1557,6 +1557,11 @@ int cdcx_decode_chunk_perm_static(cdcx_ctx* c, const uint8_t* d_payload, size_t 
                                   size_t perm_capacity, int64_t* n_perm, void* stream) {
   if (!c || !d_payload || !d_perm || !n_perm) return CDCX_ERR_ARG;
   *n_perm = 0;
+  // (the kernels read the payload as 8-byte and 4-byte words; a gzip context's payloads are zlib streams)
+  if (c->gzip || (reinterpret_cast<uintptr_t>(d_payload) & 7) || (reinterpret_cast<uintptr_t>(d_perm) & 3)) {
+    c->err = "cdcx_decode_chunk_perm_static: plain-CDC context, 8-byte aligned payload and 4-byte aligned perm required";
+    return CDCX_ERR_ARG;
+  }
   if (len == 0 || (len & 7) || len > ((size_t)1 << 40)) {
     c->err = "chunk payload length must be a positive multiple of 8";
     return CDCX_ERR_CORRUPT;

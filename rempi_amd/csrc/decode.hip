@@ -507,8 +507,9 @@ __global__ void __launch_bounds__(64) k_dec_pair_scan(const DUnit* __restrict__ 
     const uint64_t xni = wave_inclusive_scan(ai, OpAdd()), xnd = wave_inclusive_scan(ad, OpAdd());
     const uint64_t z0i = czi + zoi, z0d = czd + zod;
     uint64_t xi = cxi + 4 * czi * (uint64_t)l + (xni - ai), xd = cxd + 4 * czd * (uint64_t)l + (xnd - ad);
-    if (lists && (k & (kSegWarm - 1)) == 0 && ((k / kSegWarm) & 7) == 7) {  // k = s * kSegPairs - kSegWarm
-      const int32_t sg = (k / kSegWarm + 1) >> 3;
+    constexpr int32_t kPer = kSegPairs / kSegWarm;
+    if (lists && (k & (kSegWarm - 1)) == 0 && (k / kSegWarm) % kPer == kPer - 1) {  // k = s * kSegPairs - kSegWarm
+      const int32_t sg = (k / kSegWarm + 1) / kPer;
       if (sg < u.nseg) {
         int64_t* o = pcar + 4 * (u.seg0 + sg);
         o[0] = (int64_t)z0i;

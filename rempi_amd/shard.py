@@ -60,14 +60,15 @@ def lane_sizes(count: int, streams: int) -> list[int]:
 
 
 def reduce_counters(counters, elapsed: float, dist=None, device="cpu"):
-    """Sum the counter vector and take the max elapsed time over all processes."""
-    c = np.asarray(counters, dtype=np.float64)
+    """Sum the counter vector (whole numbers: records, bytes, ranks; kept and reduced as 64-bit
+    integers, so sums stay exact past 2^53) and take the max elapsed time over all processes."""
+    c = np.asarray(counters, dtype=np.int64)
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return c, float(elapsed)
     import torch
 
     t = torch.tensor([float(elapsed)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    v = torch.tensor(c, dtype=torch.float64, device=device)
+    v = torch.tensor(c, dtype=torch.int64, device=device)
     dist.all_reduce(v)
     return v.cpu().numpy(), float(t.item())

@@ -37,6 +37,8 @@ def lib():
         L.oracle_reconstruct.argtypes = [u8p, ctypes.c_size_t, i32p, ctypes.c_size_t, P(i32p), P(ctypes.c_size_t)]
         L.oracle_sorted_keys.argtypes = [i32p, ctypes.c_size_t, ctypes.c_int64, P(i32p), P(ctypes.c_size_t)]
         L.oracle_free.argtypes = [ctypes.c_void_p]
+        L.oracle_set_reference_walk.argtypes = [ctypes.c_int]
+        L.oracle_set_reference_walk.restype = None
         _lib = L
     return _lib
 
@@ -79,6 +81,12 @@ def decode(data: bytes) -> bytes:
     d = ctypes.string_at(out, n.value)
     L.oracle_free(out)
     return d
+
+
+def set_reference_walk(on: bool):
+    """True: delays longer than the list walk on through the sentinel as in the reference;
+    False (default): they are refused, as the device path refuses them."""
+    lib().oracle_set_reference_walk(int(on))
 
 
 def cdc_pairs(c):

@@ -192,6 +192,36 @@ def test_chain_tiers_vs_oracle(tier, monkeypatch):
     c.close()
 
 
+def test_chain_g16_first_tier_vs_oracle(monkeypatch):
+    """The 16-lane chain kernel as first tier (CDCX_CHAIN_G16: the path a context takes by itself
+    when a batch holds 2^30 rows or more, where the 8-lane kernel's 32-bit row offsets end):
+    reference bytes on random streams and on the generator workloads, with escalations."""
+    monkeypatch.setenv("CDCX_CHAIN_G16", "1")
+    c = rempi_amd.Context(131072)
+    monkeypatch.delenv("CDCX_CHAIN_G16")
+    rng = np.random.default_rng(1234)
+    bad = []
+    for t in range(40):
+        mode = ["jitter", "jitter", "jitter", "reversed", "random"][t % 5]
+        recs = S.gen_stream(int(rng.integers(1 << 30)), int(rng.integers(0, 4000)), n_sets=int(rng.integers(1, 4)),
+                            n_senders=int(rng.integers(1, 80)), jitter=int(rng.choice([0, 4, 8, 32, 200])), mode=mode)
+        want, _ = O.encode(recs, 131072)
+        got = c.encode_stream(recs)
+        if got != want:
+            bad.append((t, mode, recs.shape[0], first_diff(got, want)))
+    assert not bad, bad[:5]
+    for jitter in (8, 32, 128):
+        p = rempi_amd.default_gen_params(world_size=256, jitter=jitter, events_per_rank=150000)
+        d_rec, rec_off = c.generate_device(p, 3, 2)
+        d_out, off, ln = c.encode_batch_device(d_rec, rec_off)
+        kt = c.kernel_times()
+        for r in range(2):
+            want, _ = O.encode(rempi_amd.generate_host(p, 3 + r), 131072)
+            got = cdcx.d2h(d_out + int(off[r]), int(ln[r])).tobytes()
+            assert got == want, (jitter, r, c.chain_tiers(), first_diff(got, want))
+    c.close()
+
+
 @pytest.mark.parametrize("tier", [0, 1, 2, 3])
 def test_decode_tiers_vs_oracle(tier, monkeypatch):
     """Each permutation-rebuild tier alone (pair segments in 16-lane LDS-ring groups, whole units

@@ -28,6 +28,59 @@ def test_oracle_encode_matches_reference(name):
 def test_oracle_decode_matches_reference(name):
     d = G.load(name)
     assert O.decode(d["rempi"]) == d["tables"]
+    try:  # (and with the reference's unbounded walk: the same tables on well-formed files)
+        O.set_reference_walk(True)
+        assert O.decode(d["rempi"]) == d["tables"]
+    finally:
+        O.set_reference_walk(False)
+
+
+def _with_delays(data: bytes, table: int, delays) -> bytes:
+    """The one-chunk record file `data` with the delays of its table number `table` replaced
+    (second-order prediction re-applied, rempi_compression_util.cpp:117-154)."""
+    b = bytearray(data)
+    q = 8
+    u64 = lambda p: int(np.frombuffer(bytes(b[p:p + 8]), np.uint64)[0])  # noqa: E731
+    for k in range(table + 1):
+        q += 8
+        esz = u64(q)
+        q += 8 + 2 * esz
+        for _ in range(2):  # with_previous, matched_index: {length, bytes, data}
+            q += 16 + u64(q + 8)
+        for _ in range(2):  # unmatched ids, counts: {bytes, data}
+            q += 8 + u64(q)
+        psz = u64(q)
+        if k == table:
+            P = psz // 8
+            assert len(delays) == P
+            x = np.array([0, 0] + list(delays), np.int64)
+            y = (x[2:] - 2 * x[1:-1] + x[:-2]).astype(np.int32)
+            b[q + 8 + 4 * P:q + 8 + 8 * P] = y.tobytes()
+        q += 8 + psz
+    return bytes(b)
+
+
+@pytest.mark.skipif(not O.have_ref(), reason="needs the reference binary (oracle/_ref/ref_cdc)")
+def test_reference_walks_through_the_list_end():
+    """Delays longer than the list: the reference keeps stepping through std::list's sentinel;
+    the oracle does the same with oracle_set_reference_walk(1) and refuses them by default (the
+    device path's rule).  Pinned here against the reference decoder itself on the KAT file."""
+    d = G.load("kat")
+    tabs = O.parse_tables(d["tables"])[0]
+    M, P = tabs[0]["count"], len(tabs[0]["delays"])
+    for delays in ([2, -3, -3, -5, -8, -6], [M + 3, -3, -3, -5, -8, -6], [2, -3, -(2 * M + 5), -5, -8, 3 * M]):
+        data = _with_delays(d["rempi"], 0, delays[:P])
+        ref, _ = O.ref_decode(data)
+        try:
+            O.set_reference_walk(True)
+            assert O.decode(data) == ref, delays
+        finally:
+            O.set_reference_walk(False)
+        if max(abs(v) for v in delays) > M:
+            with pytest.raises(O.OracleError):
+                O.decode(data)
+        else:
+            assert O.decode(data) == ref
 
 
 @pytest.mark.parametrize("name", [n for n in NAMES if not G.load(n)["ref_failed"]])

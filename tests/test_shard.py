@@ -57,7 +57,7 @@ def _worker(rank, ws, port, q):
             recs += h.shape[0]
             comp += len(O.encode(h, 4096)[0])
             mine.append(r)
-    c, t = shard.reduce_counters([recs, comp, len(mine)], 1.0 + rank, dist)
+    c, t = shard.reduce_counters([recs, comp, len(mine), (1 << 53) + 1], 1.0 + rank, dist)
     q.put((rank, c.tolist(), t, mine))
     dist.destroy_process_group()
 
@@ -81,5 +81,5 @@ def test_gloo_world2_covers_the_whole_job():
         comp += len(O.encode(h, 4096)[0])
     assert sorted(r for _, _, _, mine in res for r in mine) == list(range(WORLD))  # every rank once
     for _, c, t, _ in res:
-        assert c == [float(recs), float(comp), float(WORLD)]
+        assert c == [recs, comp, WORLD, 2 * ((1 << 53) + 1)]  # (whole numbers, exact past 2^53)
         assert t == 2.0  # max over ranks

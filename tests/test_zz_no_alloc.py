@@ -1,7 +1,8 @@
 """The entry point that allocates nothing (cdcx_decode_chunk_perm_static: one chunk payload in
 device memory -> the tables' permutated indices, all scratch in the library's static device
-array) against the existing cdcx_decode_batch_device on the same chunk, bit for bit: calls in
-a row on one context, each smaller or different from the last, so stale scratch would show."""
+array) against the existing cdcx_decode_batch_device on the same chunk and against the CPU
+oracle's permutated indices, bit for bit: calls in a row on one context, each smaller or
+different from the last, so stale scratch would show."""
 import numpy as np
 import pytest
 
@@ -33,6 +34,12 @@ def perm_existing(c, data):
     return out
 
 
+def perm_oracle(data):
+    """The oracle's matched_events_permutated_indices of the file's tables, in file order."""
+    tabs = [t for chunk in O.parse_tables(O.decode(data)) for t in chunk]
+    return np.concatenate([t["perm"] for t in tabs] + [np.zeros(0, np.int64)]).astype(np.int32)
+
+
 def perm_static(c, payload, d_perm, cap):
     d = cdcx.DeviceArray(np.frombuffer(payload, np.uint8))
     n = c.decode_chunk_perm_static(d.ptr, len(payload), d_perm.ptr, cap)
@@ -61,6 +68,7 @@ def test_static_entry_point_matches_batch_decode():
         got = perm_static(c, payload, d_perm, cap)
         assert got.shape == want.shape, (k, got.shape, want.shape)
         np.testing.assert_array_equal(got, want, err_msg=f"stream {k}")
+        np.testing.assert_array_equal(got, perm_oracle(data), err_msg=f"stream {k} against the oracle")
     # limits and damage are reported, and the next call still works
     big = rempi_amd.generate_host(rempi_amd.default_gen_params(world_size=64, events_per_rank=330000), 2)
     payload, _ = payload_of(big)
@@ -75,6 +83,17 @@ def test_static_entry_point_matches_batch_decode():
         perm_static(c, small[:-8], d_perm, cap)
     assert e.value.code == 4
     np.testing.assert_array_equal(perm_static(c, small, d_perm, cap), perm_existing(c, data))
+    # arguments the kernels cannot read are refused: a payload that is not 8-byte aligned, a gzip context
+    d = cdcx.DeviceArray(np.frombuffer(b"\0\0\0\0" + small, np.uint8))
+    with pytest.raises(cdcx.CdcxError) as e:
+        c.decode_chunk_perm_static(d.ptr + 4, len(small), d_perm.ptr, cap)
+    assert e.value.code == 1
+    d.close()
+    cz = rempi_amd.Context(1 << 40, gzip=1)
+    with pytest.raises(cdcx.CdcxError) as e:
+        perm_static(cz, small, d_perm, cap)
+    assert e.value.code == 1
+    cz.close()
     # a second context on the same device shares the device's array
     c2 = rempi_amd.Context(1 << 40)
     np.testing.assert_array_equal(perm_static(c2, small, d_perm, cap), perm_existing(c, data))
