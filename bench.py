@@ -69,6 +69,8 @@ def parse(argv=None):
     ap.add_argument("--kernel-report", action="store_true", help="print per-kernel times to stderr")
     ap.add_argument("--host-io", type=int, default=1, help="steps of the copy-inclusive measurement (0 = skip)")
     ap.add_argument("--host-io-ranks", type=int, default=12, help="rank traces per lane in the copy-inclusive measurement")
+    ap.add_argument("--config2", type=int, default=1,
+                    help="also run config 2 (the CPU sample's 64 x 1M traces) on the GPU and compare its files with the CPU codec's")
     ap.add_argument("--solo", type=int, default=2, help="steps of one lane alone for the roofline figure (0 = skip)")
     return ap.parse_args(argv)
 
@@ -131,14 +133,19 @@ def cpu_baseline(args):
     nxt = [0]
     lock = threading.Lock()
 
+    file_sha = [None] * n  # SHA-256 of every rank file the CPU codec wrote (config2's byte comparison)
+
     def one(f):
         if kind == "reference":
             a = subprocess.run([O.REF_BIN, "encode", f, f + ".rempi", str(args.max_len)], capture_output=True, text=True)
             b = subprocess.run([O.REF_BIN, "decode", f + ".rempi", f + ".tables"], capture_output=True, text=True)
+            with open(f + ".rempi", "rb") as fh:
+                file_sha[files.index(f)] = hashlib.sha256(fh.read()).hexdigest()
             return float(a.stdout.split()[1]), float(b.stdout.split()[1])
         out = subprocess.run([sys.executable, os.path.abspath(__file__), "--port-one", f, str(args.max_len)],
                              capture_output=True, text=True)
-        e, d = out.stdout.split()[-2:]
+        e, d, sha = out.stdout.split()[-3:]
+        file_sha[files.index(f)] = sha
         return float(e), float(d)
 
     def work(w):
@@ -175,6 +182,7 @@ def cpu_baseline(args):
             "encode_s_per_rank": round(float(np.mean(enc_s)), 3), "decode_s_per_rank": round(float(np.mean(dec_s)), 3),
             "wall_s": round(wall, 2), "wall_gbs": round(nbytes / wall / 1e9, 4),
             "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "usable_cpus": usable_cores(),
+            "file_sha256": file_sha,
             "sample": f"config 2 in full: {n} rank traces x {args.cpu_sample_events} events of the same workload "
                       f"(world {args.world}, J={args.jitter}), {workers} worker processes; value = bytes / "
                       f"(encode + decode codec seconds of the busiest worker)"}
@@ -190,7 +198,7 @@ def port_one(f, mx):
     b, _ = O.encode(r, mx)
     t1 = time.perf_counter()
     O.decode(b)
-    print(t1 - t0, time.perf_counter() - t1)
+    print(t1 - t0, time.perf_counter() - t1, hashlib.sha256(b).hexdigest())
 
 
 # ---------------------------------------------------------------------------------------
@@ -328,6 +336,52 @@ def verify_lane(ln: Lane, fixture: dict, oracle_ranks=(), p=None, max_len=131072
                 res["enc_fail"] += 1
                 res["notes"].append(f"rank {r}: file differs from the CPU restatement's")
     return res
+
+
+def run_config2(args, device, file_sha, steps=6):
+    """Config 2 of BASELINE.json on the GPU, beside the CPU leg that runs it in full: the 64 rank
+    traces x 1M events of the same generator, one resident batch on --streams lanes, encoded and
+    decoded `steps` times (timed, device-resident), every rank verified by the device round trip,
+    and every rank file compared (SHA-256) with the one the CPU codec wrote for that rank."""
+    import torch
+
+    import rempi_amd
+    from rempi_amd import cdcx, shard
+
+    n = args.cpu_sample_ranks
+    p = rempi_amd.default_gen_params(world_size=args.world, jitter=args.jitter, events_per_rank=args.cpu_sample_events)
+    lanes = [Lane(args.max_len, device) for _ in range(max(1, min(args.streams, n)))]
+    try:
+        at = 0
+        for ln, k in zip(lanes, shard.lane_sizes(n, len(lanes))):
+            ln.load(p, at, k)
+            at += k
+        run_lanes(lanes, Lane.step, 1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run_lanes(lanes, Lane.step, steps)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        records = sum(ln.records for ln in lanes)
+        bad_rt = cmp_n = cmp_bad = 0
+        for ln in lanes:
+            d_out, off, flen, d_recs, n_out, d_perm = ln.last
+            if ln.ctx.verify_roundtrip_device(ln.d_rec, stream=ln.stream) or n_out != ln.records:
+                bad_rt += ln.n
+            for q in range(ln.n):
+                want = file_sha[ln.first + q] if file_sha else None
+                if want:
+                    cmp_n += 1
+                    cmp_bad += sha(cdcx.d2h(d_out + int(off[q]), int(flen[q]))) != want
+        return {"workload": f"config2: {n} rank traces x {args.cpu_sample_events} events (world {args.world}, J={args.jitter}), "
+                            f"one resident batch on {len(lanes)} lanes, encode+decode round trip",
+                "value": round(records * steps * RECORD_BYTES / dt / 1e9, 3), "unit": "GB/s", "steps": steps,
+                "ms_per_step": round(dt / steps * 1e3, 3), "records_per_step": records,
+                "verify": {"roundtrip_ranks": n, "roundtrip_failures": bad_rt, "files_compared_with_cpu_codec": cmp_n,
+                           "file_failures": int(cmp_bad)}}
+    finally:
+        for ln in lanes:
+            ln.close()
 
 
 # ---------------------------------------------------------------------------------------
@@ -510,9 +564,16 @@ def main():
             print("  verify:", note, file=sys.stderr)
 
     # (after the last collective: with several GPU processes only rank 0 is still busy here)
-    cpu = None
+    cpu = cfg2 = None
     if args.cpu_baseline and rank == 0:
         cpu = cpu_baseline(args)
+    if args.config2 and rank == 0:
+        for ln in lanes:  # (their buffers hold most of the HBM)
+            ln.close()
+        lanes = []
+        cfg2 = run_config2(args, local, (cpu or {}).get("file_sha256"))
+    if cpu:
+        cpu.pop("file_sha256", None)
 
     if rank == 0:
         ranks_done = int(counters[6])
@@ -564,6 +625,7 @@ def main():
                          "pipeline_valu_per_record": None if traffic is None else traffic.get("pipeline_valu_per_record")},
             "cpu_baseline": cpu,
             "host_io": host_io,
+            "configs": {"config2": cfg2},
         }
         print(json.dumps(out))
     for ln in lanes:

@@ -12,7 +12,9 @@
  *               size_t matched_index[], size_t uid_bytes, size_t LP(unmatched_id)[],
  *               size_t ucnt_bytes, size_t unmatched_count[], size_t pair_bytes,
  *               int32 LP(ids)[], int32 LP(deltas)[]
- *   footer    = size_t n, int32 ranks[n] (all_epoch_rank_uset order), int32 0
+ *   footer    = size_t n, int32 ranks[n] (all_epoch_rank_uset order), int32 L,
+ *               size_t msg_ids[L], int32 set_ids[L] (the matching-set-id map in
+ *               unordered_map<size_t,int> order; L = 0 unless a map was registered)
  *
  * Input records: the reference's 8 x int32 test event (rempi_event.h:40-48):
  *   [0] event_count [1] type [2] flag [3] rank [4] with_next [5] index [6] clock
@@ -291,6 +293,48 @@ int cdcx_replay_decode_files(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_fil
 typedef int (*cdcx_replay_table_sink)(void* user, int32_t file_index, size_t n_chunks, const cdcx_tables* chunks);
 int cdcx_replay_decode_tables(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths,
                               int64_t batch_bytes, cdcx_replay_table_sink sink, void* user, cdcx_replay_stats* stats);
+
+/* ---------------------------------------------------------------------------------------
+ * Footer contents (write_footer :2085-2126, read_footer :2015-2083).
+ */
+
+/* rempi_reqmg_set_matching_set_id_map (rempi_request_mg.cpp:1136-1143): register message id ->
+ * matching set id entries on the context, in this order; an id registered before keeps its
+ * place and takes the new set id (unordered_map operator[]).  n == 0 forgets all entries.
+ * The rank files written by the host-buffer entry points of this context (cdcx_encode_stream,
+ * cdcx_transcode_basic) then end with the map as write_footer emits it -- int32 L,
+ * size_t msg_ids[L], int32 set_ids[L], in the iteration order of the reference's
+ * unordered_map<size_t, int> comm_tag_to_matching_set_id (rempi_request_mg.cpp:1083-1094).
+ * The device-resident batch path always writes L = 0 (the map is host state of a recording
+ * process, not trace data). */
+int cdcx_set_matching_set_id_map(cdcx_ctx* ctx, const uint64_t* msg_ids, const int32_t* set_ids, size_t n);
+
+/* write_footer with a map: as cdcx_footer, plus the n_ids map entries given in registration
+ * order.  Same length protocol as cdcx_footer. */
+int cdcx_footer_ex(const int32_t* epoch_ranks, size_t n_ranks, const uint64_t* msg_ids, const int32_t* set_ids,
+                   size_t n_ids, uint8_t* out, size_t* len);
+
+/* read_footer: the footer of a rank file image (plain or REMPI_GZIP=1: the footer is stored
+ * plain either way): the global predecessor ranks in file order (the reference reads and drops
+ * them, :2044-2054) and the matching-set-id map in file order, as read_footer hands it to
+ * rempi_reqmg_set_matching_set_id_map (:2057-2073).  *out is one block: cdcx_free(*out).
+ * CDCX_ERR_CORRUPT for a file without separator or with a footer shorter than it says. */
+typedef struct cdcx_footer_info {
+  size_t n_ranks;
+  const int32_t* ranks;
+  size_t n_ids;
+  const uint64_t* msg_ids;
+  const int32_t* set_ids;
+} cdcx_footer_info;
+int cdcx_read_footer(const uint8_t* file, size_t len, cdcx_footer_info** out);
+
+/* cdcx_replay_decode_tables that also delivers every file's footer: footer_sink(user, i, info)
+ * is called (serialised with the table sink, right before file i's tables) with the parsed
+ * footer of file i, valid during the call.  footer_sink may be NULL. */
+typedef int (*cdcx_replay_footer_sink)(void* user, int32_t file_index, const cdcx_footer_info* footer);
+int cdcx_replay_decode_tables_ex(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths,
+                                 int64_t batch_bytes, cdcx_replay_table_sink sink, cdcx_replay_footer_sink footer_sink,
+                                 void* user, cdcx_replay_stats* stats);
 
 /* ---------------------------------------------------------------------------------------
  * Synthetic workload (definition in DESIGN.md "Synthetic traces"), generated

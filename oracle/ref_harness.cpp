@@ -22,6 +22,16 @@
 //        read_record_file + decode per chunk (rempi_encoder_cdc.cpp:933-1299), dumping the
 //        decoded tables (int64 little-endian, layout in oracle/tables_format.md).
 //        Prints "decode_s <seconds>".
+//   REF_CDC_IDMAP=<file> ref_cdc encode ...
+//        before the footer is written, registers the matching-set-id map of <file> (L x
+//        {uint64 msg id, int64 set id}) with the reference's own
+//        rempi_reqmg_set_matching_set_id_map (rempi_request_mg.cpp:1136-1143), entry by entry in
+//        file order, so that write_footer (:2105-2121) emits it.
+//   ref_cdc footer <in.rempi> <out.map>
+//        constructs the encoder in replay mode -- its constructor runs read_footer (:2015-2083),
+//        which feeds the footer's map back through rempi_reqmg_set_matching_set_id_map -- and
+//        dumps what rempi_reqmg_get_matching_set_id_map (:1068-1096) then returns: int64 L,
+//        L msg ids, L set ids.
 #include <mpi.h>
 #include <chrono>
 #include <cstdio>
@@ -33,6 +43,7 @@
 #include "rempi_event_list.h"
 #include "rempi_config.h"
 #include "rempi_event.h"
+#include "rempi_request_mg.h"
 
 namespace {
 double now_s() {
@@ -79,6 +90,17 @@ int do_encode(const char* in, const char* out, int max_len, int gzip, int rep) {
     enc.encode();
     enc.write_record_file();
     // The reference's write_queue_vec points into fmt; it is consumed by write_record_file.
+  }
+  if (const char* mapf = getenv("REF_CDC_IDMAP")) {
+    FILE* mf = fopen(mapf, "rb");
+    if (!mf) { perror(mapf); return 2; }
+    int64_t e[2];
+    while (fread(e, sizeof e, 1, mf) == 1) {
+      size_t id = (size_t)e[0];
+      int sid = (int)e[1];
+      rempi_reqmg_set_matching_set_id_map(&id, &sid, 1);
+    }
+    fclose(mf);
   }
   enc.close_record_file();
   double t1 = now_s();
@@ -168,9 +190,28 @@ int do_decode(const char* in, const char* out, int gzip) {
   printf("decode_s %.6f chunks %lld\n", total, (long long)chunks);
   return 0;
 }
+int do_footer(const char* in, const char* out) {
+  rempi_mode = 1;
+  rempi_gzip = 0;
+  Dec dec(in);  // (read_footer runs in the constructor)
+  size_t* ids = nullptr;
+  int* sets = nullptr;
+  int L = 0;
+  rempi_reqmg_get_matching_set_id_map(&ids, &sets, &L);
+  FILE* f = fopen(out, "wb");
+  if (!f) { perror(out); return 2; }
+  Dump d{f};
+  d.v(L);
+  for (int i = 0; i < L; i++) d.v((int64_t)ids[i]);
+  for (int i = 0; i < L; i++) d.v(sets[i]);
+  fclose(f);
+  printf("footer_map %d\n", L);
+  return 0;
+}
 }  // namespace
 
 int main(int argc, char** argv) {
+  if (argc >= 4 && std::string(argv[1]) == "footer") return do_footer(argv[2], argv[3]);
   if (argc >= 5 && std::string(argv[1]) == "encode")
     return do_encode(argv[2], argv[3], atoi(argv[4]), argc >= 6 && std::string(argv[5]) == "gzip",
                      argc >= 6 && std::string(argv[5]) == "rep");

@@ -74,6 +74,14 @@ _REPLAY_SINK = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.c_int32, _i64p, ctypes
 
 _REPLAY_TABLE_SINK = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.c_int32, ctypes.c_size_t, P(Tables))
 
+
+class FooterInfo(ctypes.Structure):
+    _fields_ = [("n_ranks", ctypes.c_size_t), ("ranks", _i32p), ("n_ids", ctypes.c_size_t),
+                ("msg_ids", P(ctypes.c_uint64)), ("set_ids", _i32p)]
+
+
+_REPLAY_FOOTER_SINK = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.c_int32, P(FooterInfo))
+
 _SIGNATURES = {
     "cdcx_create": ([P(_Opts)], _vp),
     "cdcx_destroy": ([_vp], None),
@@ -93,6 +101,12 @@ _SIGNATURES = {
     "cdcx_decode_chunk": ([_vp, _u8p, ctypes.c_size_t, P(Tables)], ctypes.c_int),
     "cdcx_reconstruct_chunk": ([_vp, _u8p, ctypes.c_size_t, _i32p, ctypes.c_size_t, P(_i32p), P(ctypes.c_size_t)], ctypes.c_int),
     "cdcx_footer": ([_i32p, ctypes.c_size_t, _u8p, P(ctypes.c_size_t)], ctypes.c_int),
+    "cdcx_footer_ex": ([_i32p, ctypes.c_size_t, P(ctypes.c_uint64), _i32p, ctypes.c_size_t, _u8p, P(ctypes.c_size_t)],
+                       ctypes.c_int),
+    "cdcx_set_matching_set_id_map": ([_vp, P(ctypes.c_uint64), _i32p, ctypes.c_size_t], ctypes.c_int),
+    "cdcx_read_footer": ([_u8p, ctypes.c_size_t, P(P(FooterInfo))], ctypes.c_int),
+    "cdcx_replay_decode_tables_ex": ([P(_vp), ctypes.c_int32, ctypes.c_int32, P(ctypes.c_char_p), ctypes.c_int64,
+                                      _REPLAY_TABLE_SINK, _REPLAY_FOOTER_SINK, _vp, P(ReplayStats)], ctypes.c_int),
     "cdcx_decode_batch_device": ([_vp, ctypes.c_int32, _vp, _i64p, _i64p, _vp, ctypes.c_int64, P(_vp), _i64p, P(_vp), _vp], ctypes.c_int),
     "cdcx_decode_chunk_perm_static": ([_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _i64p, _vp], ctypes.c_int),
     "cdcx_decode_rank_offsets": ([_vp, ctypes.c_int32, _i64p, _i64p], ctypes.c_int),
@@ -179,19 +193,50 @@ def gunzip_file(data: bytes) -> bytes:
     return _zlib_stage(lib().cdcx_gunzip_file, data)
 
 
-def footer(epoch_ranks) -> bytes:
-    """write_footer's bytes for the epoch ranks inserted in this order (cdcx_footer; host only)."""
+def footer(epoch_ranks, msg_ids=None, set_ids=None) -> bytes:
+    """write_footer's bytes for the epoch ranks inserted in this order and, optionally, the
+    matching-set-id map registered in this order (cdcx_footer / cdcx_footer_ex; host only)."""
     L = lib()
     r = np.ascontiguousarray(epoch_ranks, dtype=np.int32)
     n = ctypes.c_size_t(0)
-    rc = L.cdcx_footer(_ptr(r, ctypes.c_int32), r.size, None, ctypes.byref(n))
+    if msg_ids is None:
+        call = lambda out: L.cdcx_footer(_ptr(r, ctypes.c_int32), r.size, out, ctypes.byref(n))  # noqa: E731
+    else:
+        m = np.ascontiguousarray(msg_ids, dtype=np.uint64)
+        q = np.ascontiguousarray(set_ids, dtype=np.int32)
+        assert m.size == q.size
+        call = lambda out: L.cdcx_footer_ex(_ptr(r, ctypes.c_int32), r.size, _ptr(m, ctypes.c_uint64),  # noqa: E731
+                                            _ptr(q, ctypes.c_int32), m.size, out, ctypes.byref(n))
+    rc = call(None)
     if rc:
         raise CdcxError(rc, "footer size")
     out = np.zeros(n.value, np.uint8)
-    rc = L.cdcx_footer(_ptr(r, ctypes.c_int32), r.size, _ptr(out, ctypes.c_uint8), ctypes.byref(n))
+    rc = call(_ptr(out, ctypes.c_uint8))
     if rc:
         raise CdcxError(rc, "footer")
     return out[: n.value].tobytes()
+
+
+def _footer_dict(fi) -> dict:
+    def arr(ptr, n, dt):
+        return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dt).copy() if n else np.zeros(0, dt)
+
+    return {"ranks": arr(fi.ranks, fi.n_ranks, np.int32), "msg_ids": arr(fi.msg_ids, fi.n_ids, np.uint64),
+            "set_ids": arr(fi.set_ids, fi.n_ids, np.int32)}
+
+
+def read_footer(data: bytes) -> dict:
+    """read_footer of a rank file image: {"ranks", "msg_ids", "set_ids"} in file order
+    (cdcx_read_footer; host only)."""
+    L = lib()
+    buf = np.frombuffer(data, dtype=np.uint8)
+    out = P(FooterInfo)()
+    rc = L.cdcx_read_footer(_ptr(buf, ctypes.c_uint8), buf.size, ctypes.byref(out))
+    if rc:
+        raise CdcxError(rc, "read_footer")
+    d = _footer_dict(out.contents)
+    L.cdcx_free(out)
+    return d
 
 
 class Context:
@@ -206,6 +251,15 @@ class Context:
         if not self._c:
             raise CdcxError(5, f"cdcx_create failed (device {device})")
         self.max_event_length = max_event_length
+
+    def set_matching_set_id_map(self, msg_ids=(), set_ids=()):
+        """rempi_reqmg_set_matching_set_id_map: entries the files written by encode_stream /
+        transcode_basic then carry in their footer; no entries = forget the map."""
+        m = np.ascontiguousarray(msg_ids, dtype=np.uint64)
+        q = np.ascontiguousarray(set_ids, dtype=np.int32)
+        assert m.size == q.size
+        self._check(lib().cdcx_set_matching_set_id_map(self._c, _ptr(m, ctypes.c_uint64), _ptr(q, ctypes.c_int32), m.size),
+                    "set_matching_set_id_map")
 
     def close(self):
         if getattr(self, "_c", None):
@@ -527,11 +581,13 @@ def _table_dict(x: Table) -> dict:
             "perm": arr(x.perm, x.count, np.int32)}
 
 
-def replay_decode_tables(contexts, paths, sink=None, batch_bytes: int = 0, convert: bool = True) -> dict:
+def replay_decode_tables(contexts, paths, sink=None, batch_bytes: int = 0, convert: bool = True, footer_sink=None) -> dict:
     """Streaming replay decode delivering flat tables (cdcx_replay_decode_tables).  sink(file_index,
     chunks) gets, per file, a list (chunks) of lists (tables, ascending set id) of dicts -- copies
     of the arrays, which only live during the C callback; with convert=False the sink gets
-    (file_index, n_chunks, pointer to cdcx_tables) and must not keep the pointer."""
+    (file_index, n_chunks, pointer to cdcx_tables) and must not keep the pointer.
+    footer_sink(file_index, {"ranks", "msg_ids", "set_ids"}) gets every file's footer right
+    before its tables (cdcx_replay_decode_tables_ex)."""
     L = lib()
     ctxs = (_vp * len(contexts))(*[c._c for c in contexts])
     enc = [os.fsencode(p) for p in paths]
@@ -550,9 +606,21 @@ def replay_decode_tables(contexts, paths, sink=None, batch_bytes: int = 0, conve
             failure.append(e)
             return 1
 
+    def _fsink(_user, i, fi):
+        try:
+            return 1 if footer_sink(int(i), _footer_dict(fi.contents)) else 0
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            failure.append(e)
+            return 1
+
     cb = _REPLAY_TABLE_SINK(_sink)
     st = ReplayStats()
-    rc = L.cdcx_replay_decode_tables(ctxs, len(contexts), len(enc), arr, int(batch_bytes), cb, None, ctypes.byref(st))
+    if footer_sink is None:
+        rc = L.cdcx_replay_decode_tables(ctxs, len(contexts), len(enc), arr, int(batch_bytes), cb, None, ctypes.byref(st))
+    else:
+        fcb = _REPLAY_FOOTER_SINK(_fsink)
+        rc = L.cdcx_replay_decode_tables_ex(ctxs, len(contexts), len(enc), arr, int(batch_bytes), cb, fcb, None,
+                                            ctypes.byref(st))
     if failure:
         raise failure[0]
     if rc:

@@ -220,6 +220,9 @@ struct cdcx_ctx {
                                 getenv("CDCX_GATE_SCATTER") ? atoi(getenv("CDCX_GATE_SCATTER")) : 1};
   hipEvent_t gate_ev[kGateKinds][4] = {};
   int gate_next[kGateKinds] = {};
+  // matching-set-id map (cdcx_set_matching_set_id_map), registration order, ids distinct
+  std::vector<uint64_t> map_ids;
+  std::vector<int32_t> map_sets;
   int64_t chain_tier_counts[3] = {0, 0, 0};  // segments entering each tier in the last encode
   int64_t dec_tier_counts[7] = {0, 0, 0, 0, 0, 0, 0};  // tables entering each rebuild tier in the last decode; segments
 
@@ -377,6 +380,8 @@ int guarded(cdcx_ctx* c, F&& f) {
 }
 
 inline unsigned blocks(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+void append_id_map(const cdcx_ctx* c, std::vector<uint8_t>& file);  // (with the footer code below)
 
 // Grow-only page-locked host buffer.
 uint8_t* pinned(cdcx_ctx::Pinned& b, size_t bytes) {
@@ -1190,6 +1195,7 @@ int cdcx_encode_stream(cdcx_ctx* c, const int32_t* rec8, size_t n, uint8_t** out
     std::vector<uint8_t> h(fl[0]);
     HIPCHK(hipMemcpyAsync(h.data(), c->d_out + fo[0], fl[0], hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    append_id_map(c, h);
     if (c->gzip) h = gzip_file(h.data(), h.size());
     *out = host_copy(h);
     *out_len = h.size();
@@ -1248,6 +1254,7 @@ int cdcx_transcode_basic(cdcx_ctx* c, size_t nf, const uint8_t* const* files, co
     }
     HIPCHK(hipStreamSynchronize(s));
     for (size_t f = 0; f < nf; f++) {
+      append_id_map(c, h[f]);
       if (c->gzip) h[f] = gzip_file(h[f].data(), h[f].size());
       outs[f] = host_copy(h[f]);
       out_lens[f] = h[f].size();
@@ -1451,37 +1458,191 @@ int cdcx_reconstruct_chunk(cdcx_ctx* c, const uint8_t* payload, size_t len, cons
   });
 }
 
-int cdcx_footer(const int32_t* epoch_ranks, size_t n_in, uint8_t* out, size_t* len) {
-  if ((n_in && !epoch_ranks) || !len || n_in > (size_t)INT32_MAX - 1) return CDCX_ERR_ARG;
-  try {
-    // std::unordered_set<int>: identity hash of the sign-extended int (hash_order.h)
-    std::vector<uint64_t> key(n_in + 1);
-    std::vector<int32_t> next(n_in + 1), bucket(hash_bucket_capacity(n_in) + 1);
-    HashOrder h;
-    h.init(key.data(), next.data(), bucket.data());
-    for (size_t i = 0; i < n_in; i++) {
-      const uint64_t k = (uint64_t)(int64_t)epoch_ranks[i];
-      if (!h.contains(k)) h.insert_new(k);
+}  // extern "C"
+
+namespace {
+
+// Keys in the iteration order of a libstdc++ unordered container with identity hash after
+// inserting them in the given order (hash_order.h); positions of the first insertions.
+std::vector<size_t> hash_iteration_order(const std::vector<uint64_t>& keys_in_order) {
+  const size_t n = keys_in_order.size();
+  std::vector<uint64_t> key(n + 1);
+  std::vector<int32_t> next(n + 1), bucket(hash_bucket_capacity(n) + 1);
+  std::vector<size_t> first;  // node -> index of its first insertion
+  HashOrder h;
+  h.init(key.data(), next.data(), bucket.data());
+  for (size_t i = 0; i < n; i++)
+    if (!h.contains(keys_in_order[i])) {
+      h.insert_new(keys_in_order[i]);
+      first.push_back(i);
     }
-    const size_t need = 8 + 8 + 4 * (size_t)h.size + 4;
+  std::vector<size_t> out;
+  for (int32_t p = h.head; p != -1; p = h.next[p]) out.push_back(first[p]);
+  return out;
+}
+
+// write_footer (rempi_encoder_cdc.cpp:2085-2126): separator, distinct ranks in
+// unordered_set<int> order, the matching-set-id map in unordered_map<size_t,int> order.
+std::vector<uint8_t> footer_bytes(const int32_t* epoch_ranks, size_t n_in, const uint64_t* msg_ids, const int32_t* set_ids,
+                                  size_t n_ids) {
+  std::vector<uint64_t> rk(n_in);
+  for (size_t i = 0; i < n_in; i++) rk[i] = (uint64_t)(int64_t)epoch_ranks[i];  // std::hash<int>: the sign-extended value
+  const std::vector<size_t> ro = hash_iteration_order(rk);
+  // the map: a later entry of an id overwrites the set id and keeps the id's node
+  std::vector<uint64_t> ids(msg_ids, msg_ids + n_ids);
+  const std::vector<size_t> mo = hash_iteration_order(ids);
+  std::map<uint64_t, int32_t> last;
+  for (size_t i = 0; i < n_ids; i++) last[msg_ids[i]] = set_ids[i];
+  std::vector<uint8_t> out(16 + 4 * ro.size() + 4 + 12 * mo.size());
+  uint64_t v = 0;
+  memcpy(out.data(), &v, 8);
+  v = ro.size();
+  memcpy(out.data() + 8, &v, 8);
+  size_t q = 16;
+  for (size_t i : ro) {
+    memcpy(out.data() + q, &epoch_ranks[i], 4);
+    q += 4;
+  }
+  const int32_t L = (int32_t)mo.size();
+  memcpy(out.data() + q, &L, 4);
+  q += 4;
+  for (size_t i : mo) {
+    memcpy(out.data() + q, &msg_ids[i], 8);
+    q += 8;
+  }
+  for (size_t i : mo) {
+    const int32_t sid = last[msg_ids[i]];
+    memcpy(out.data() + q, &sid, 4);
+    q += 4;
+  }
+  return out;
+}
+
+// A rank file as the device wrote it (footer ending in int32 0) with the context's map appended.
+void append_id_map(const cdcx_ctx* c, std::vector<uint8_t>& file) {
+  if (c->map_ids.empty() || file.size() < 4) return;
+  const std::vector<uint8_t> f = footer_bytes(nullptr, 0, c->map_ids.data(), c->map_sets.data(), c->map_ids.size());
+  file.resize(file.size() - 4);                        // the device's int32 0
+  file.insert(file.end(), f.begin() + 16, f.end());    // int32 L, ids, set ids
+}
+
+struct FooterView {
+  size_t n_ranks = 0, n_ids = 0;
+  const uint8_t* ranks = nullptr;    // int32[n_ranks], maybe unaligned
+  const uint8_t* msg_ids = nullptr;  // size_t[n_ids]
+  const uint8_t* set_ids = nullptr;  // int32[n_ids]
+};
+// read_footer (rempi_encoder_cdc.cpp:2015-2083): skip the chunks, then parse.
+bool parse_footer(const uint8_t* b, size_t len, FooterView* fv) {
+  size_t p = 0;
+  while (true) {
+    if (len - p < 8) return false;
+    uint64_t n;
+    memcpy(&n, b + p, 8);
+    p += 8;
+    if (n == 0) break;
+    if (n > len - p) return false;
+    p += n;
+  }
+  if (len - p < 8) return false;
+  uint64_t nr;
+  memcpy(&nr, b + p, 8);
+  p += 8;
+  if (nr > (len - p) / 4) return false;
+  fv->n_ranks = nr;
+  fv->ranks = b + p;
+  p += 4 * nr;
+  if (len - p < 4) return false;
+  int32_t L;
+  memcpy(&L, b + p, 4);
+  p += 4;
+  if (L > 0) {
+    if ((uint64_t)L > (len - p) / 12) return false;
+    fv->n_ids = (size_t)L;
+    fv->msg_ids = b + p;
+    fv->set_ids = b + p + 8 * (size_t)L;
+  }
+  return true;
+}
+// One malloc block: the struct, then 8-aligned copies of the arrays.
+cdcx_footer_info* footer_info_block(const FooterView& fv) {
+  const size_t head = (sizeof(cdcx_footer_info) + 15) / 16 * 16;
+  const size_t bytes = head + 8 * fv.n_ids + 4 * fv.n_ids + 4 * fv.n_ranks + 16;
+  uint8_t* blk = static_cast<uint8_t*>(malloc(bytes));
+  if (!blk) throw std::bad_alloc();
+  cdcx_footer_info* fi = reinterpret_cast<cdcx_footer_info*>(blk);
+  uint8_t* ids = blk + head;
+  uint8_t* sets = ids + 8 * fv.n_ids;
+  uint8_t* ranks = sets + 4 * fv.n_ids;
+  if (fv.n_ids) memcpy(ids, fv.msg_ids, 8 * fv.n_ids);
+  if (fv.n_ids) memcpy(sets, fv.set_ids, 4 * fv.n_ids);
+  if (fv.n_ranks) memcpy(ranks, fv.ranks, 4 * fv.n_ranks);
+  fi->n_ranks = fv.n_ranks;
+  fi->ranks = reinterpret_cast<const int32_t*>(ranks);
+  fi->n_ids = fv.n_ids;
+  fi->msg_ids = reinterpret_cast<const uint64_t*>(ids);
+  fi->set_ids = reinterpret_cast<const int32_t*>(sets);
+  return fi;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cdcx_footer_ex(const int32_t* epoch_ranks, size_t n_in, const uint64_t* msg_ids, const int32_t* set_ids, size_t n_ids,
+                   uint8_t* out, size_t* len) {
+  if ((n_in && !epoch_ranks) || (n_ids && (!msg_ids || !set_ids)) || !len || n_in > (size_t)INT32_MAX - 1 ||
+      n_ids > (size_t)INT32_MAX - 1)
+    return CDCX_ERR_ARG;
+  try {
+    const std::vector<uint8_t> f = footer_bytes(epoch_ranks, n_in, msg_ids, set_ids, n_ids);
     if (out) {
-      if (*len < need) {
-        *len = need;
+      if (*len < f.size()) {
+        *len = f.size();
         return CDCX_ERR_ARG;
       }
-      uint64_t v = 0;
-      memcpy(out, &v, 8);
-      v = (uint64_t)h.size;
-      memcpy(out + 8, &v, 8);
-      size_t q = 16;
-      for (int32_t p = h.head; p != -1; p = h.next[p], q += 4) {
-        const int32_t r = (int32_t)(int64_t)h.key[p];
-        memcpy(out + q, &r, 4);
-      }
-      const int32_t zero = 0;
-      memcpy(out + q, &zero, 4);
+      memcpy(out, f.data(), f.size());
     }
-    *len = need;
+    *len = f.size();
+    return CDCX_OK;
+  } catch (const std::bad_alloc&) {
+    return CDCX_ERR_NOMEM;
+  }
+}
+
+int cdcx_footer(const int32_t* epoch_ranks, size_t n_in, uint8_t* out, size_t* len) {
+  return cdcx_footer_ex(epoch_ranks, n_in, nullptr, nullptr, 0, out, len);
+}
+
+int cdcx_set_matching_set_id_map(cdcx_ctx* c, const uint64_t* msg_ids, const int32_t* set_ids, size_t n) {
+  if (!c || (n && (!msg_ids || !set_ids))) return CDCX_ERR_ARG;
+  try {
+    if (n == 0) {
+      c->map_ids.clear();
+      c->map_sets.clear();
+    }
+    for (size_t i = 0; i < n; i++) {
+      const auto it = std::find(c->map_ids.begin(), c->map_ids.end(), msg_ids[i]);
+      if (it != c->map_ids.end()) {
+        c->map_sets[it - c->map_ids.begin()] = set_ids[i];
+      } else {
+        c->map_ids.push_back(msg_ids[i]);
+        c->map_sets.push_back(set_ids[i]);
+      }
+    }
+    return CDCX_OK;
+  } catch (const std::bad_alloc&) {
+    return CDCX_ERR_NOMEM;
+  }
+}
+
+int cdcx_read_footer(const uint8_t* file, size_t len, cdcx_footer_info** out) {
+  if (!file || !out) return CDCX_ERR_ARG;
+  *out = nullptr;
+  try {
+    FooterView fv;
+    if (!parse_footer(file, len, &fv)) return CDCX_ERR_CORRUPT;
+    *out = footer_info_block(fv);
     return CDCX_OK;
   } catch (const std::bad_alloc&) {
     return CDCX_ERR_NOMEM;
@@ -1686,6 +1847,7 @@ struct ReplayJob {
   std::mutex sink_mu;
   cdcx_replay_sink sink = nullptr;              // int64 dumps, or
   cdcx_replay_table_sink table_sink = nullptr;  // flat tables pointing into the pinned buffers
+  cdcx_replay_footer_sink footer_sink = nullptr;  // ... preceded by the file's parsed footer
   void* user;
   std::atomic<int64_t> chunks{0}, units{0}, records{0}, bytes{0}, dump_bytes{0};
   std::atomic<int64_t> ns_read{0}, ns_device{0}, ns_dump{0}, ns_sink{0};  // thread time per phase
@@ -1796,6 +1958,15 @@ void replay_batch(cdcx_ctx* c, ReplayJob& job, int32_t b, hipStream_t s) {
       job.ns_dump += ns_since(t);
       std::lock_guard<std::mutex> g(job.sink_mu);
       if (job.stop) return;
+      if (job.footer_sink) {
+        FooterView fv;
+        if (!parse_footer(h + off[r], (size_t)len[r], &fv))
+          throw CdcxError{CDCX_ERR_CORRUPT, "no footer in rank file " + std::to_string(f0 + r)};
+        cdcx_footer_info* fi = footer_info_block(fv);
+        const int rc = job.footer_sink(job.user, f0 + r, fi);
+        free(fi);
+        if (rc != 0) throw CdcxError{CDCX_ERR_ARG, "replay sink stopped the pipeline at file " + std::to_string(f0 + r)};
+      }
       if (job.table_sink(job.user, f0 + r, chunks.size(), chunks.data()) != 0)
         throw CdcxError{CDCX_ERR_ARG, "replay sink stopped the pipeline at file " + std::to_string(f0 + r)};
       job.ns_sink += ns_since(t);
@@ -1826,7 +1997,8 @@ extern "C" {
 
 namespace {
 int replay_run(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths, int64_t batch_bytes,
-               cdcx_replay_sink sink, cdcx_replay_table_sink table_sink, void* user, cdcx_replay_stats* stats);
+               cdcx_replay_sink sink, cdcx_replay_table_sink table_sink, cdcx_replay_footer_sink footer_sink, void* user,
+               cdcx_replay_stats* stats);
 }
 
 extern "C" {
@@ -1834,13 +2006,20 @@ extern "C" {
 int cdcx_replay_decode_files(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths,
                              int64_t batch_bytes, cdcx_replay_sink sink, void* user, cdcx_replay_stats* stats) {
   if (!sink) return CDCX_ERR_ARG;
-  return replay_run(ctxs, n_ctx, n_files, paths, batch_bytes, sink, nullptr, user, stats);
+  return replay_run(ctxs, n_ctx, n_files, paths, batch_bytes, sink, nullptr, nullptr, user, stats);
 }
 
 int cdcx_replay_decode_tables(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths,
                               int64_t batch_bytes, cdcx_replay_table_sink sink, void* user, cdcx_replay_stats* stats) {
   if (!sink) return CDCX_ERR_ARG;
-  return replay_run(ctxs, n_ctx, n_files, paths, batch_bytes, nullptr, sink, user, stats);
+  return replay_run(ctxs, n_ctx, n_files, paths, batch_bytes, nullptr, sink, nullptr, user, stats);
+}
+
+int cdcx_replay_decode_tables_ex(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths,
+                                 int64_t batch_bytes, cdcx_replay_table_sink sink, cdcx_replay_footer_sink footer_sink,
+                                 void* user, cdcx_replay_stats* stats) {
+  if (!sink) return CDCX_ERR_ARG;
+  return replay_run(ctxs, n_ctx, n_files, paths, batch_bytes, nullptr, sink, footer_sink, user, stats);
 }
 
 }  // extern "C"
@@ -1848,7 +2027,8 @@ int cdcx_replay_decode_tables(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_fi
 namespace {
 
 int replay_run(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char* const* paths, int64_t batch_bytes,
-               cdcx_replay_sink sink, cdcx_replay_table_sink table_sink, void* user, cdcx_replay_stats* stats) {
+               cdcx_replay_sink sink, cdcx_replay_table_sink table_sink, cdcx_replay_footer_sink footer_sink, void* user,
+               cdcx_replay_stats* stats) {
   if (!ctxs || n_ctx <= 0 || n_files < 0 || (n_files && !paths)) return CDCX_ERR_ARG;
   for (int32_t i = 0; i < n_ctx; i++) {
     if (!ctxs[i]) return CDCX_ERR_ARG;
@@ -1863,6 +2043,7 @@ int replay_run(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n_files, const char
   job.paths = paths;
   job.sink = sink;
   job.table_sink = table_sink;
+  job.footer_sink = footer_sink;
   job.user = user;
   job.size.resize(n_files);
   for (int32_t i = 0; i < n_files; i++) {

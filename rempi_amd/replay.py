@@ -55,10 +55,11 @@ def decode_dir(rempi_dir: str, streams: int = 4, batch_bytes: int = 256 << 20, g
 
 def decode_dir_tables(rempi_dir: str, streams: int = 4, batch_bytes: int = 256 << 20, gzip: int = 0, device: int = 0,
                       sink=None, ranks: range | None = None, max_event_length: int = 131072, convert: bool = True,
-                      devices=None):
+                      devices=None, footer_sink=None):
     """Like decode_dir, but sink(rank, chunks) gets the flat tables of every chunk (what the
     reference's replay engine consumes) instead of an int64 dump.  `devices`: one device ordinal
-    per context (contexts of one call may sit on different GPUs)."""
+    per context (contexts of one call may sit on different GPUs).  footer_sink(rank, footer) gets
+    every file's footer (global predecessor ranks, matching-set-id map) before its tables."""
     files = rank_files(rempi_dir, ranks)
     devs = list(devices) if devices else [device] * max(streams, 1)
     ctxs = [cdcx.Context(max_event_length=max_event_length, device=d, gzip=gzip) for d in devs]
@@ -66,7 +67,8 @@ def decode_dir_tables(rempi_dir: str, streams: int = 4, batch_bytes: int = 256 <
         fwd = None
         if sink is not None:
             fwd = (lambda i, *rest: sink(files[i][0], *rest))
-        st = cdcx.replay_decode_tables(ctxs, [p for _, p in files], fwd, batch_bytes, convert)
+        ffwd = None if footer_sink is None else (lambda i, footer: footer_sink(files[i][0], footer))
+        st = cdcx.replay_decode_tables(ctxs, [p for _, p in files], fwd, batch_bytes, convert, ffwd)
     finally:
         for c in ctxs:
             c.close()

@@ -69,3 +69,16 @@ def load_rep(name):
     for k in ("rempi_rep", "tables"):
         d[k] = d[k].tobytes()
     return d
+
+
+def footer_names():
+    """Fixtures of the footer's matching-set-id map (tests/golden/make_footer_golden.py)."""
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "footer_*.npz")))
+
+
+def load_footer(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    d["max_len"] = int(d["max_len"])
+    d["rempi"] = d["rempi"].tobytes()
+    return d

@@ -154,3 +154,52 @@ def test_replay_rejects_a_context_passed_twice(tmp_path):
         cdcx.replay_decode_files([c, c], [p for _, p in replay.rank_files(str(tmp_path))])
     assert e.value.code == 1
     c.close()
+
+
+@pytest.mark.gpu
+def test_replay_1024_files_over_4_contexts(tmp_path):
+    """1024 small rank files of the bench workload through four contexts in small batches: every
+    file's tables arrive once, and their permutated indices are the ones cdcx_decode_batch_device
+    gives for the same file right after encoding; two of the files also against the oracle."""
+    import hashlib
+
+    import rempi_amd
+
+    n_files, per = 1024, 128
+    p = cdcx.default_gen_params(world_size=1024, events_per_rank=3000)
+    ctx = cdcx.Context()
+    want, keep = {}, {}
+    for b0 in range(0, n_files, per):
+        d_rec, rec_off = ctx.generate_device(p, b0, per)
+        d_out, off, ln = ctx.encode_batch_device(d_rec, rec_off)
+        img = cdcx.d2h(d_out, int(off[-1] + ln[-1]))
+        _, _, d_perm = ctx.decode_batch_device(d_out, off, ln)
+        _, po = ctx.decode_rank_offsets(per)
+        perm = cdcx.d2h(d_perm, int(po[-1]) * 4, np.int32)
+        for i in range(per):
+            data = img[off[i]:off[i] + ln[i]].tobytes()
+            (tmp_path / f"rank_{b0 + i}.rempi").write_bytes(data)
+            want[b0 + i] = hashlib.sha256(memoryview(np.ascontiguousarray(perm[po[i]:po[i + 1]]))).hexdigest()
+            if b0 + i in (5, 777):
+                keep[b0 + i] = data
+    ctx.close()
+    got = {}
+
+    def sink(rank, chunks):
+        assert rank not in got
+        h = hashlib.sha256()
+        for tabs in chunks:
+            for t in tabs:
+                h.update(memoryview(np.ascontiguousarray(t["perm"], dtype=np.int32)))
+        got[rank] = h.hexdigest()
+
+    st, ranks = replay.decode_dir_tables(str(tmp_path), streams=4, batch_bytes=3 << 20, sink=sink)
+    assert st["files"] == n_files and st["batches"] >= 8 and ranks == list(range(n_files))
+    assert got == want
+    for r, data in keep.items():
+        assert data == O.encode(rempi_amd.generate_host(p, r), 131072)[0]
+        h = hashlib.sha256()
+        for chunk in O.parse_tables(O.decode(data)):
+            for t in chunk:
+                h.update(memoryview(np.ascontiguousarray(t["perm"], dtype=np.int32)))
+        assert h.hexdigest() == want[r]

@@ -9,18 +9,24 @@ r * WORLD_SIZE // R == RANK (contiguous blocks, SURVEY §8(e)); no collective.
     python tools/replay_bench.py --ranks 4096 --events 100000 --dir /tmp/rempi_dir
 """
 import argparse
+import hashlib
 import json
 import os
 import shutil
 import sys
 import time
 
+import numpy as np
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from rempi_amd import cdcx, replay  # noqa: E402
 
 
-def write_dir(d, ranks, world, events, batch, device):
+def write_dir(d, ranks, world, events, batch, device, perm_sha=None):
+    """Encode the ranks' synthetic traces on the GPU into d/rank_<r>.rempi.  perm_sha (a dict):
+    also decode every batch right there (cdcx_decode_batch_device) and keep the SHA-256 of each
+    rank's permutated indices, for the check of what the replay pipeline delivers later."""
     ctx = cdcx.Context(device=device)
     s = cdcx.stream_create()
     p = cdcx.default_gen_params(world_size=world, events_per_rank=events)
@@ -36,6 +42,12 @@ def write_dir(d, ranks, world, events, batch, device):
                 with open(os.path.join(d, f"rank_{b0 + i}.rempi"), "wb") as f:
                     f.write(img[off[i]:off[i] + ln[i]].tobytes())
             total += int(rec_off[-1])
+            if perm_sha is not None:
+                _, _, d_perm = ctx.decode_batch_device(d_out, off, ln, stream=s)
+                _, po = ctx.decode_rank_offsets(n)
+                perm = cdcx.d2h(d_perm, int(po[-1]) * 4, np.int32)
+                for i in range(n):
+                    perm_sha[b0 + i] = hashlib.sha256(memoryview(np.ascontiguousarray(perm[po[i]:po[i + 1]]))).hexdigest()
     finally:
         ctx.close()
     return total
@@ -51,6 +63,9 @@ def main():
     ap.add_argument("--gen-batch", type=int, default=64)
     ap.add_argument("--repeat", type=int, default=2, help="decode passes (the first warms up)")
     ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--verify", type=int, default=1,
+                    help="after the timed passes, one more pass that hashes every file's delivered permutated indices "
+                         "against the encoder-side decode of the same file")
     ap.add_argument("--py-sink", action="store_true", help="hand every dump to a Python sink (bytes copy)")
     ap.add_argument("--tables", action="store_true",
                     help="deliver flat tables per chunk (cdcx_replay_decode_tables) instead of int64 dumps")
@@ -62,7 +77,8 @@ def main():
     d = f"{a.dir}_{rank}"
     os.makedirs(d, exist_ok=True)
     t0 = time.perf_counter()
-    records = write_dir(d, range(lo, hi), a.ranks, a.events, a.gen_batch, dev)
+    perm_sha = {} if a.verify else None
+    records = write_dir(d, range(lo, hi), a.ranks, a.events, a.gen_batch, dev, perm_sha)
     t_write = time.perf_counter() - t0
     n_dumped = [0]
 
@@ -83,6 +99,28 @@ def main():
             st, _ = replay.decode_dir_tables(d, a.streams, a.batch_mb << 20, 0, dev, table_sink, convert=False)
         else:
             st, _ = replay.decode_dir(d, a.streams, a.batch_mb << 20, 0, dev, sink if a.py_sink else None)
+    # Untimed: every file's permutated indices as the pipeline delivers them, hashed and compared
+    # with the encoder-side decode of the same file (write_dir).
+    verify = None
+    if a.verify:
+        seen, bad = set(), []
+
+        def check_sink(r, n_chunks, chunks):
+            h = hashlib.sha256()
+            for k in range(n_chunks):
+                for q in range(chunks[k].n_tables):
+                    t = chunks[k].tables[q]
+                    if t.count:
+                        h.update(memoryview(np.ctypeslib.as_array(t.perm, shape=(t.count,))))
+            seen.add(r)
+            if h.hexdigest() != perm_sha.get(r):
+                bad.append(r)
+
+        replay.decode_dir_tables(d, a.streams, a.batch_mb << 20, 0, dev, check_sink, convert=False)
+        missing = sorted(set(perm_sha) - seen)
+        verify = {"files_checked": len(seen), "files_failed": len(bad) + len(missing), "failed_ranks": (bad + missing)[:16],
+                  "how": "SHA-256 of each file's permutated indices from the table sink against "
+                         "cdcx_decode_batch_device of the same file right after it was encoded"}
     if not a.keep:
         shutil.rmtree(d, ignore_errors=True)
     out = {
@@ -98,6 +136,7 @@ def main():
         "file_gbps": round(st["file_bytes"] / st["seconds"] / 1e9, 2),
         "dump_gb": round(st["dump_bytes"] / 1e9, 3), "py_sink_dumps": n_dumped[0],
         "thread_s": {k: round(st[k], 3) for k in ("read_s", "device_s", "dump_s", "sink_s")},
+        "verify": verify,
     }
     print(json.dumps(out), flush=True)
 
