@@ -224,6 +224,7 @@ struct cdcx_ctx {
   std::vector<uint64_t> map_ids;
   std::vector<int32_t> map_sets;
   int64_t chain_tier_counts[3] = {0, 0, 0};  // segments entering each tier in the last encode
+  int32_t chain_cnt0[4] = {0, 0, 0, 0};      // (host image of the tiers' counters at launch)
   int64_t dec_tier_counts[7] = {0, 0, 0, 0, 0, 0, 0};  // tables entering each rebuild tier in the last decode; segments
 
   template <class T>
@@ -435,9 +436,9 @@ const std::vector<Unit>& host_enc_units(cdcx_ctx* c, hipStream_t s) {
 // Outputs: c->d_out with the rank files at file_off[r] (16-aligned), file_len[r].
 //
 // The work lists between the kernels (chunks, units, sort tiles, segment offsets, output
-// layout) are built on the device (lists.hip).  The host waits four times, each time for a
-// few hundred bytes: the chunk and table counts of the ranks, the unit / segment totals, the
-// chain tiers' hand-over counts, and the file offsets with the error word at the end.
+// layout) are built on the device (lists.hip).  The host waits three times, each time for a
+// few hundred bytes: the chunk and table counts of the ranks, the unit / segment totals, and
+// the file offsets with the error word (and the chain tiers' hand-over counts) at the end.
 void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* rec_off_h, std::vector<int64_t>& file_off,
                   std::vector<int64_t>& file_len, hipStream_t s) {
   const int64_t N = rec_off_h[R];
@@ -682,12 +683,14 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   // Tiers: 8-lane groups with 16 leaf slots; segments whose leaf list outgrows them go to
   // 64-lane groups, then to the lane kernel's exact global-memory path.  Each tier rewrites
   // every output of the segments it takes.
+  // (two words per record and unit: the edit sequence later, the lane tier's leaf lists before that)
+  uint32_t* d_seq = c->buf<uint32_t>("seq", 2 * (size_t)(N + lbn));
   int32_t* d_cnt = c->buf<int32_t>("chain_cnt", 4);
   int32_t* d_ovf1 = c->buf<int32_t>("chain_ovf1", nsegs);
   int32_t* d_ovf2 = c->buf<int32_t>("chain_ovf2", nsegs);
   {
-    const int32_t cnt0[4] = {(int32_t)nsegs, 0, 0, 0};
-    HIPCHK(hipMemcpyAsync(d_cnt, cnt0, sizeof(cnt0), hipMemcpyHostToDevice, s));
+    c->chain_cnt0[0] = (int32_t)nsegs;
+    HIPCHK(hipMemcpyAsync(d_cnt, c->chain_cnt0, sizeof(c->chain_cnt0), hipMemcpyHostToDevice, s));
     const int32_t* list = d_segord;
     const int32_t* nlist = d_cnt;
     int64_t n = nsegs;
@@ -706,30 +709,23 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
       list = d_ovf1;
       nlist = d_cnt + 1;
     }
-    // The 64-lane tier reads its segment count from the device (d_cnt + 1), so the host
-    // waits once, after it (wait 3); only the rare lane tier needs the count on the host.
+    // Every tier reads the number of segments handed to it from the device (d_cnt), so the host
+    // does not wait between them; the counts travel back with the file layout at the end.
     if (c->chain_tier <= 1) {
       const int64_t g64 = c->chain_tier <= 0 ? std::min<int64_t>(1024, blocks(nsegs, 4)) : blocks(n, 4);
       c->launch(K_CHAIN_G64, k_chain_grp<64>, dim3((unsigned)std::max<int64_t>(1, g64)), dim3(256), s,
                 (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,
                 d_topg, d_qn, d_ovf2, d_cnt + 2, d_err);
       list = d_ovf2;
+      nlist = d_cnt + 2;
     }
-    {
-      Mail m(c, s, 64);
-      const size_t o = m.add(d_cnt, 12);
-      const int32_t* cnt = reinterpret_cast<const int32_t*>(m.wait() + o);
-      c->chain_tier_counts[0] = nsegs;
-      c->chain_tier_counts[1] = c->chain_tier <= 0 ? cnt[1] : nsegs;
-      if (c->chain_tier <= 1) n = cnt[2];
-    }
-    int2* d_leaves = n > 0 ? c->buf<int2>("leaves", tot.w1n) : nullptr;  // lane tier only
-    if (n > 0)
-      c->launch(K_CHAIN_SEG, k_chain_seg<16>, dim3((unsigned)std::min<int64_t>(1024, blocks(n, 256))), dim3(256), s,
-                (const Unit*)d_units, d_segs, (int32_t)n, list, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par,
-                d_exta, d_topg, d_qn, d_leaves, (const int64_t*)d_w1, d_err,
-                c->chain_stats ? c->buf<unsigned long long>("chain_stats", 8) : (unsigned long long*)nullptr);
-    c->chain_tier_counts[2] = n;
+    // The lane tier's exact leaf lists live in the edit sequence's buffer, which is written later.
+    int2* d_leaves = reinterpret_cast<int2*>(d_seq);
+    c->launch(K_CHAIN_SEG, k_chain_seg<16>,
+              dim3((unsigned)(c->chain_tier >= 2 ? std::max<int64_t>(1, std::min<int64_t>(1024, blocks(nsegs, 256))) : 16)),
+              dim3(256), s, (const Unit*)d_units, d_segs, nlist, list, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par,
+              d_exta, d_topg, d_qn, d_leaves, (const int64_t*)d_w1, d_err,
+              c->chain_stats ? c->buf<unsigned long long>("chain_stats", 8) : (unsigned long long*)nullptr);
   }
   int32_t* d_qexit = c->buf<int32_t>("qexit", N);
   c->launch(K_CHAIN_EXITS, k_chain_exits, dim3((unsigned)std::min<int64_t>(8192, blocks(nsegs, 256))), dim3(256), s,
@@ -742,7 +738,6 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   out_layout();  // (the pair counts are final: k_chain_entries)
   int32_t* d_posA = c->buf<int32_t>("posA", N);
   int32_t* d_crow = c->buf<int32_t>("crow", N);
-  uint32_t* d_seq = c->buf<uint32_t>("seq", 2 * N);
   int32_t* d_sx = c->buf<int32_t>("sx", 2 * N);
   c->launch_gated(2, NU >= 4096 && (c->gate_bw & 16), K_POSITIONS, k_pos_rows, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_cord,
             (const uint8_t*)d_chain, d_posA, d_crow);
@@ -760,11 +755,18 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   c->launch(K_FOOTER_WRITE, k_footer_write, dim3(blocks(R, 64)), dim3(64), s, (const int64_t*)d_fk_off,
             (const int64_t*)d_fb_off, (const uint64_t*)d_fkey, (const int32_t*)d_fnext, (const int32_t*)d_fbucket,
             (const int32_t*)d_fcount, (const int64_t*)(d_files + 2 * R), R, d_out);
-  {  // wait 4: error word, file offsets and lengths
-    Mail m(c, s, 64 + 8 * (3 * (size_t)R + 1));
+  {  // wait 3: error word, file offsets and lengths, the chain tiers' counts
+    Mail m(c, s, 128 + 8 * (3 * (size_t)R + 1));
     const size_t o_err = m.add(d_err, 4), o_f = m.add(d_files, 8 * (3 * (size_t)R + 1));
+    const size_t o_cnt = m.add(c->rep ? (const void*)d_err : (const void*)c->buf<int32_t>("chain_cnt", 4), c->rep ? 4 : 12);
     const uint8_t* h = m.wait();
     raise_device_error(*reinterpret_cast<const uint32_t*>(h + o_err));
+    if (!c->rep) {
+      const int32_t* cnt = reinterpret_cast<const int32_t*>(h + o_cnt);
+      c->chain_tier_counts[0] = cnt[0];
+      c->chain_tier_counts[1] = c->chain_tier <= 0 ? cnt[1] : cnt[0];
+      c->chain_tier_counts[2] = c->chain_tier <= 1 ? cnt[2] : cnt[0];
+    }
     const int64_t* f = reinterpret_cast<const int64_t*>(h + o_f);
     file_off.assign(f, f + R);
     file_len.assign(f + R, f + 2 * R);

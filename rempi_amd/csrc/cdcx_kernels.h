@@ -48,7 +48,7 @@ __global__ void k_seg_hist(const Seg*, int32_t, int32_t*);
 __global__ void k_seg_bins(int32_t*);
 __global__ void k_seg_order(const Seg*, int32_t, int32_t*, int32_t*);
 template <int NL>
-__global__ void k_chain_seg(const Unit*, Seg*, int32_t, const int32_t*, const int32_t*, const int32_t*, int32_t*,
+__global__ void k_chain_seg(const Unit*, Seg*, const int32_t*, const int32_t*, const int32_t*, const int32_t*, int32_t*,
                             int32_t*, int32_t*, int32_t*, int2*, const int64_t*, uint32_t*, unsigned long long*);
 template <int G>
 __global__ void k_chain_grp(const Unit*, Seg*, const int32_t*, const int32_t*, const int32_t*, const int32_t*, int32_t*,

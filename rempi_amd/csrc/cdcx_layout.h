@@ -88,7 +88,7 @@ struct DUnit {
 // Pair segments of the permutation rebuild (decode.hip): the pair list of a unit is cut every
 // kSegPairs pairs; a segment replays the kSegWarm pairs before its own from the untouched list
 // first, and its state then is checked against the state its predecessor ends in.
-constexpr int32_t kSegPairs = 1024;   // pairs per segment (multiple of 8 * kSegWarm)
+constexpr int32_t kSegPairs = 2048;   // pairs per segment (multiple of 8 * kSegWarm)
 constexpr int32_t kSegWarm = 128;     // pairs replayed before a segment's own (multiple of 32)
 constexpr int32_t kSegDelta = 32;     // a segment's positions start this far below its smallest pair id
 constexpr int32_t kSegWin = 128;      // list positions compared between neighbouring segments (= the window)

@@ -185,7 +185,8 @@ struct Stream4 {
 }  // namespace
 
 template <int NL>
-__global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ units, Seg* __restrict__ segs, int32_t nsegs,
+__global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ units, Seg* __restrict__ segs,
+                                                   const int32_t* __restrict__ nsegs_p,
                                                    const int32_t* __restrict__ order, const int32_t* __restrict__ cord,
                                                    const int32_t* __restrict__ opn, int32_t* __restrict__ par,
                                                    int32_t* __restrict__ exta, int32_t* __restrict__ topg,
@@ -201,6 +202,7 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
   __shared__ int32_t next_j;
   if (threadIdx.x == 0) next_j = 0;
   __syncthreads();
+  const int32_t nsegs = *nsegs_p;  // (a count left on the device by the tier before: the host does not wait for it)
   int32_t si = -1;
   int64_t a = 0, lbase = 0;
   int32_t s0 = 0, s1 = 0, ord = 0;
@@ -423,7 +425,7 @@ __global__ void __launch_bounds__(256) k_chain_seg(const Unit* __restrict__ unit
   }
 }
 
-template __global__ void k_chain_seg<16>(const Unit*, Seg*, int32_t, const int32_t*, const int32_t*, const int32_t*,
+template __global__ void k_chain_seg<16>(const Unit*, Seg*, const int32_t*, const int32_t*, const int32_t*, const int32_t*,
                                          int32_t*, int32_t*, int32_t*, int32_t*, int2*, const int64_t*, uint32_t*,
                                          unsigned long long*);
 

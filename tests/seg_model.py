@@ -13,7 +13,7 @@ are then compared with the same positions of the state its predecessor ended in.
 from __future__ import annotations
 
 W, AHEAD = 128, 56            # window slots, room kept behind an untouched id
-PAIRS, WARM, DELTA = 1024, 128, 32
+PAIRS, WARM, DELTA = 2048, 128, 32
 MAXP = 262144
 NOCAP = 0x7FFFFFF0
 

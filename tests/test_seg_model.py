@@ -44,20 +44,22 @@ def test_segments_vs_sequential_replay(reach, expect_pass):
 
 
 def test_rerun_on_bench_trace():
-    """One table of rank 317 of the bench workload (400 K events) has a segment whose replay gives
-    another state than its predecessor ends in; run again from that state the table comes out as
-    the sequential replay's.  (tests/test_gpu_parity.py runs the same trace on the device.)"""
+    """Ranks 317 and 446 of the bench workload (400 K events) each have a table with a segment
+    whose replay gives another state than its predecessor ends in (rank 317 with segments of 1024
+    pairs, rank 446 with 2048); run again from that state the table comes out as the sequential
+    replay's.  (tests/test_gpu_parity.py runs the same traces on the device.)"""
     import rempi_amd
 
     p = rempi_amd.default_gen_params(world_size=1024, events_per_rank=400_000)
-    data, _ = O.encode(rempi_amd.generate_host(p, 317), 131072)
     reruns = 0
-    for chunk in O.parse_tables(O.decode(data)):
-        for t in chunk:
-            stats = {}
-            got = SM.rebuild(t["ids"], t["delays"], t["count"], stats)
-            assert got is not None and got == [int(v) for v in t["perm"]]
-            reruns += stats.get("reruns", 0)
+    for rank in (317, 446):
+        data, _ = O.encode(rempi_amd.generate_host(p, rank), 131072)
+        for chunk in O.parse_tables(O.decode(data)):
+            for t in chunk:
+                stats = {}
+                got = SM.rebuild(t["ids"], t["delays"], t["count"], stats)
+                assert got is not None and got == [int(v) for v in t["perm"]]
+                reruns += stats.get("reruns", 0)
     assert reruns >= 1
 
 
