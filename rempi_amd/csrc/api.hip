@@ -33,7 +33,7 @@ enum KernelId {
   K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_RANK_SCAN,
   K_CHUNKS, K_UNITS_LB, K_LISTS, K_UNIT_PREP, K_WINDOW_RANK, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_G8, K_CHAIN_G16, K_CHAIN_G64, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
   K_WRITE_UNITS, K_CHUNK_HEADERS, K_FOOTER_ORDER, K_FOOTER_WRITE, K_WRITE_KEYS,
-  K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_PAIRS, K_DEC_SEG, K_DEC_LANES, K_DEC_CHECK, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS, K_DEC_PACK, K_VERIFY,
+  K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_PAIRS, K_DEC_SEG, K_DEC_CHECK, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS, K_DEC_PACK, K_VERIFY,
   K_GEN_TILE_SUMS, K_GEN_RANK_SCAN, K_GEN_FRAMES, K_GEN_AKEYS, K_GEN_ARRIVAL, K_GEN_RECORDS,
   K_COUNT
 };
@@ -41,7 +41,7 @@ const char* kKernelNames[K_COUNT] = {
   "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_rank_scan",
   "k_chunks", "k_units_lb", "k_lists", "k_unit_prep", "k_window_rank", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp8", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
-  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_pair_scan", "k_dec_perm_seg", "k_dec_perm_lanes", "k_dec_perm_check", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records", "k_dec_pack_tables", "k_verify_roundtrip",
+  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_pair_scan", "k_dec_perm_seg", "k_dec_perm_check", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records", "k_dec_pack_tables", "k_verify_roundtrip",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
 
 struct HipError {
@@ -201,8 +201,6 @@ struct cdcx_ctx {
   // First permutation-rebuild tier (diagnostics / tests): 0 = pair segments in 16-lane groups,
   // 1 = whole units in 16-lane groups, 2 = 256-slot window, 3 = sequential list.
   int dec_tier = getenv("CDCX_DEC_TIER") ? atoi(getenv("CDCX_DEC_TIER")) : 0;
-  // first tier of the rebuild: 1 = one pair segment per lane (decode_lanes.hip), 0 = per 16-lane group
-  int dec_lanes = getenv("CDCX_DEC_LANES") ? atoi(getenv("CDCX_DEC_LANES")) : 0;
   // 1: every unit takes the tile sort (skips the windowed rank), for tests
   int rank_tier = getenv("CDCX_RANK_TIER") ? atoi(getenv("CDCX_RANK_TIER")) : 0;
   // blocks of the 16-lane chain tier (a work queue: fewer blocks leave CUs to other streams)
@@ -882,13 +880,9 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
   int32_t* d_dump_w = c->buf<int32_t>("d_dump_w", (size_t)nsegs * kSegWin);
   c->launch(K_DEC_PAIRS, k_dec_pair_scan, dim3(NU), dim3(64), s, (const DUnit*)d_units, d_in, 1 | (pairs ? 4 : 0), d_segs,
             d_pcar, d_idd, d_dld);
-  if (c->dec_lanes)
-    c->launch_gated(1, NU >= 4096, K_DEC_LANES, k_dec_perm_lanes, dim3(blocks(nsegs, 64)), dim3(64), s, d_units,
-                    (const DSeg*)d_segs, nsegs, d_in, (const int64_t*)d_pcar, d_cinv, d_dump_t, d_dump_w, d_nfail);
-  else
-    c->launch_gated(1, NU >= 4096, K_DEC_SEG, k_dec_perm_seg<1>, dim3(blocks(nsegs, 4)), dim3(64), s, d_units,
-                    (const int32_t*)nullptr, (const DSeg*)d_segs, nsegs, 0, d_in, (const int64_t*)d_pcar, d_perm, d_cinv,
-                    d_dump_t, d_dump_w, d_nfail);
+  c->launch_gated(1, NU >= 4096, K_DEC_SEG, k_dec_perm_seg<1>, dim3(blocks(nsegs, 4)), dim3(64), s, d_units,
+                  (const int32_t*)nullptr, (const DSeg*)d_segs, nsegs, 0, d_in, (const int64_t*)d_pcar, d_perm, d_cinv,
+                  d_dump_t, d_dump_w, d_nfail);
   // Segments that did not start from their predecessor's final state (a few in 10^5 on the bench
   // traces) run again from that state, twice if the first rerun changed what a neighbour started
   // from; what still differs then sends its unit to the next tier.
@@ -907,9 +901,8 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
                   (const DSeg*)d_segs, (int64_t)kRedoCap, 0, d_in, (const int64_t*)d_pcar, d_perm, d_cinv, d_dump_t,
                   d_dump_w, d_nfail);
     }
-  // (the lane kernel writes cinv only: perm of every first-tier unit is read off it)
-  c->launch(K_DEC_CHECK, k_dec_perm_inv, dim3(NU), dim3(256), s, (const DUnit*)d_units,
-            c->dec_lanes ? (const int32_t*)nullptr : (const int32_t*)d_redone, (const int32_t*)d_cinv, d_perm);
+  c->launch(K_DEC_CHECK, k_dec_perm_inv, dim3(NU), dim3(256), s, (const DUnit*)d_units, (const int32_t*)d_redone,
+            (const int32_t*)d_cinv, d_perm);
   // The record tiles are listed while the rebuild runs; the reconstruction itself is launched
   // before the wait for the failure count when no unit can have failed into a later tier.
   int4* d_rt = nullptr;

@@ -106,9 +106,7 @@ __global__ void k_dec_perm_seg(DUnit*, const int32_t*, const DSeg*, int64_t, int
 __global__ void k_dec_perm_check(DUnit*, const DSeg*, int64_t, const int32_t*, const int32_t*, int32_t*, int32_t, int32_t*,
                                  int32_t*);
 __global__ void k_dec_perm_inv(const DUnit*, const int32_t*, const int32_t*, int32_t*);
-// decode_lanes.hip
-__global__ void k_dec_perm_lanes(DUnit*, const DSeg*, int64_t, const uint8_t*, const int64_t*, int32_t*, int32_t*, int32_t*,
-                                 int32_t*);
+
 __global__ void k_dec_cinv(const DUnit*, const int32_t*, int32_t*);
 template <int K>
 __global__ void k_dec_perm_window(DUnit*, int32_t, int32_t, const uint64_t*, const uint64_t*, int32_t*, int32_t*);

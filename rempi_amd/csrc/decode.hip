@@ -943,7 +943,7 @@ __global__ void __launch_bounds__(256) k_dec_perm_check(DUnit* __restrict__ unit
 
 __global__ void __launch_bounds__(256) k_dec_perm_inv(const DUnit* __restrict__ units, const int32_t* __restrict__ redone,
                                                       const int32_t* __restrict__ cinv, int32_t* __restrict__ perm) {
-  if (redone && !redone[blockIdx.x]) return;  // (redone null: every unit of the first tier)
+  if (!redone[blockIdx.x]) return;
   const DUnit u = units[blockIdx.x];
   if (u.fb != 0) return;  // (a later tier rewrites both arrays)
   for (int32_t i = threadIdx.x; i < u.M; i += 256) perm[u.key_off + cinv[u.key_off + i]] = i;
