@@ -54,7 +54,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--world", type=int, default=1024, help="ranks in the traced job")
     ap.add_argument("--events", type=int, default=10_000_000, help="events per rank trace")
-    ap.add_argument("--ranks-per-gpu", type=int, default=96, help="rank traces resident per GPU (one batch)")
+    ap.add_argument("--ranks-per-gpu", type=int, default=128, help="rank traces resident per GPU (one batch)")
     ap.add_argument("--jitter", type=int, default=8)
     ap.add_argument("--max-len", type=int, default=131072, help="REMPI_MAX")
     ap.add_argument("--streams", type=int, default=4, help="lanes of a batch in flight per GPU (one HIP stream each)")
@@ -69,8 +69,9 @@ def parse(argv=None):
     ap.add_argument("--kernel-report", action="store_true", help="print per-kernel times to stderr")
     ap.add_argument("--host-io", type=int, default=1, help="steps of the copy-inclusive measurement (0 = skip)")
     ap.add_argument("--host-io-ranks", type=int, default=12, help="rank traces per lane in the copy-inclusive measurement")
-    ap.add_argument("--config2", type=int, default=1,
-                    help="also run config 2 (the CPU sample's 64 x 1M traces) on the GPU and compare its files with the CPU codec's")
+    ap.add_argument("--config2", type=int, default=-1,
+                    help="also run config 2 (the CPU sample's 64 x 1M traces) on the GPU and compare its files with the CPU "
+                         "codec's (default: when the CPU baseline runs)")
     ap.add_argument("--solo", type=int, default=2, help="steps of one lane alone for the roofline figure (0 = skip)")
     return ap.parse_args(argv)
 
@@ -232,6 +233,9 @@ class Lane:
         d_recs, n_out, d_perm = c.decode_batch_device(d_out, off, ln, d_keys, n_keys, stream=self.stream)
         self.comp += int(ln.sum())
         self.last = (d_out, off, ln, d_recs, n_out, d_perm)
+
+    def totals(self):
+        return self.ctx.encode_totals()
 
     def host_io_step(self, pin_rec, pin_files, pin_recs):
         """Copy-inclusive: records H2D from pinned host memory, encode + decode, rank files
@@ -416,9 +420,10 @@ def main():
     p = rempi_amd.default_gen_params(world_size=args.world, jitter=args.jitter, events_per_rank=args.events)
     fixture = load_fixture(args) if args.verify else {}
     lanes = [Lane(args.max_len, local) for _ in range(max(1, min(args.streams, args.ranks_per_gpu)))]
+    n_lanes = len(lanes)
 
     elapsed = 0.0
-    n_records = comp_bytes = 0
+    n_records = comp_bytes = n_matched = n_pairs = 0
     ver = {"enc_ranks": 0, "enc_fail": 0, "dec_ranks": 0, "dec_fail": 0, "notes": []}
     ktimes = {}
     per_launch_records = 0
@@ -448,6 +453,9 @@ def main():
             ln.ctx.set_profiling(False)
             n_records += ln.records
             comp_bytes += ln.comp
+            t = ln.totals()
+            n_matched += t["matched"]
+            n_pairs += t["pairs"]
         per_launch_records = max(per_launch_records, max(ln.records for ln in active))
         if args.verify:
             for ln in active:
@@ -505,11 +513,13 @@ def main():
 
     counters, tmax = shard.reduce_counters(
         [n_records * args.steps, comp_bytes, ver["enc_ranks"], ver["enc_fail"], ver["dec_ranks"], ver["dec_fail"],
-         count if args.max_batches <= 0 else sum(n for _, n in plan)], elapsed, dist,
+         count if args.max_batches <= 0 else sum(n for _, n in plan), n_records, n_matched, n_pairs], elapsed, dist,
         "cuda" if backend == "nccl" else "cpu")
     total_records = counters[0]
     value = total_records * RECORD_BYTES / tmax / 1e9
     comp_per_event = counters[1] / max(total_records, 1)
+    # matched events per record and (id, delay) pairs per matched event, from the encoders' own totals
+    mix = Mix(m=counters[8] / max(counters[7], 1), pairs=counters[9] / max(counters[8], 1), c=comp_per_event)
 
     # Roofline of the dominant kernel: algorithmic bytes per launch / mean launch duration.
     # Dominant = the longest launch with the GPU to itself (the solo steps); with all lanes in
@@ -518,9 +528,9 @@ def main():
     traffic = pmc_traffic() if rank == 0 else None
 
     def line(k, launch_ms, launch_records):
-        algo = algorithmic_bytes(k, launch_records, comp_per_event)
+        algo = algorithmic_bytes(k, launch_records, mix)
         d = {"kernel": k, "launch_ms": round(launch_ms, 3), "algorithmic_bytes_per_launch": None, "achieved": None,
-             "frac": None}
+             "frac": None, "bound": KERNEL_BOUND.get(k, "hbm")}
         if algo is not None:  # (kernels that touch a data-dependent part of the batch have no per-record figure)
             ach = algo / (launch_ms / 1e3) / 1e9
             d.update({"algorithmic_bytes_per_launch": round(algo), "achieved": round(ach, 2),
@@ -554,7 +564,7 @@ def main():
             so = solo.get(k)
             print(f"  {k:22s} {ms / max(n, 1):10.3f} ms/launch x{n:5d}  {100 * ms / tot:5.1f}%"
                   + (f"   alone {so[0] / so[1]:8.3f} ms" if so else ""), file=sys.stderr)
-        print(f"  timed {elapsed:.3f}s for {args.steps} steps x {len(plan)} batches on {len(lanes)} streams; "
+        print(f"  timed {elapsed:.3f}s for {args.steps} steps x {len(plan)} batches on {n_lanes} streams; "
               f"kernels sum {tot / 1e3:.3f}s; job wall {job_wall:.1f}s", file=sys.stderr)
         print(f"  chain tiers of the last encode of lane 0 (segments: all, past 16 leaves, past 64): "
               f"{lanes[0].ctx.chain_tiers()}", file=sys.stderr)
@@ -567,7 +577,7 @@ def main():
     cpu = cfg2 = None
     if args.cpu_baseline and rank == 0:
         cpu = cpu_baseline(args)
-    if args.config2 and rank == 0:
+    if (args.config2 if args.config2 >= 0 else args.cpu_baseline) and rank == 0:
         for ln in lanes:  # (their buffers hold most of the HBM)
             ln.close()
         lanes = []
@@ -596,7 +606,7 @@ def main():
                        "job_ranks": args.world, "ranks_processed": ranks_done, "batches_per_gpu": len(plan),
                        "ranks_per_batch": args.ranks_per_gpu, "events_per_rank": args.events,
                        "records_per_step": int(total_records / args.steps),
-                       "jitter": args.jitter, "rempi_max": args.max_len, "streams_per_gpu": len(lanes),
+                       "jitter": args.jitter, "rempi_max": args.max_len, "streams_per_gpu": n_lanes,
                        "compressed_bytes_per_event": round(comp_per_event, 3),
                        "hbm_used_gb": round((total_b - free_b) / 1e9, 1), "hbm_total_gb": round(total_b / 1e9, 1),
                        "parallelism": f"dp{ws}: rank r -> GPU floor(r*{ws}/{args.world}), independent rank traces",
@@ -606,9 +616,12 @@ def main():
                                          "permutation for fixture ranks; encode: reference SHA-256 of the rank file "
                                          "for fixture ranks (+ CPU restatement bytes for --oracle-ranks)"},
                        "verify_failures": int(counters[3] + counters[5])},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": dom_line["achieved"], "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "bound_note": "the fraction is against the HBM roofline as the contract asks; what limits "
+                                                       "this kernel by itself is `limited_by` (vector-instruction issue: see "
+                                                       "valu_issue_frac; latency: dependent steps of few waves)",
+                         "limited_by": KERNEL_BOUND.get(dom, "hbm"), "kernel": dom, "achieved": dom_line["achieved"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": dom_line["frac"], "traffic": dom_line.get("traffic"),
-                         "traffic_source": PMC_TRAFFIC if traffic else None,
+                         "traffic_source": traffic.get("source") if traffic else None,
                          "launch_ms": round(launch_ms, 3),
                          "launch_ms_how": "HIP events, one lane alone on the GPU" if solo else
                                           "HIP events with all lanes in flight",
@@ -619,8 +632,10 @@ def main():
                                            f"{SCLK_HZ / 1e9} GHz) / launch time: the share of the launch its vector "
                                            "instructions need at the issue rate of one per 4 cycles per SIMD",
                          "kernels": top,
-                         "pipeline_achieved": round(pipeline_bytes(comp_per_event) * total_records / tmax / 1e9, 2),
-                         "pipeline_algorithmic_bytes_per_record": round(pipeline_bytes(comp_per_event), 2),
+                         "mix": {"matched_per_record": round(mix.m, 4), "pairs_per_matched": round(mix.pairs, 4),
+                                 "compressed_bytes_per_record": round(mix.c, 3)},
+                         "pipeline_achieved": round(pipeline_bytes(mix) * total_records / tmax / 1e9, 2),
+                         "pipeline_algorithmic_bytes_per_record": round(pipeline_bytes(mix), 2),
                          "pipeline_traffic_per_record": None if traffic is None else traffic.get("pipeline_bytes_per_record"),
                          "pipeline_valu_per_record": None if traffic is None else traffic.get("pipeline_valu_per_record")},
             "cpu_baseline": cpu,
@@ -634,14 +649,28 @@ def main():
         dist.destroy_process_group()
 
 
-# Algorithmic HBM bytes per input record for each kernel (DESIGN.md §3 kernel tables); m =
-# matched fraction, c = compressed bytes per record.  The dominant kernel's figure is the
-# roofline numerator.
-M_FRAC = 0.833  # gen.h: one unmatched poll before 20 % of the calls -> 1 / 1.2 matched
+# Algorithmic HBM bytes per input record for each kernel (DESIGN.md §3 kernel tables), from the
+# run's own mix: m = matched events per record, p = (id, delay) pairs per matched event, c =
+# compressed bytes per record.  The dominant kernel's figure is the roofline numerator.
+class Mix:
+    def __init__(self, m, pairs, c):
+        self.m, self.pairs, self.c = float(m), float(pairs), float(c)
 
 
-def algorithmic_bytes(kernel, n_records, c):
-    m = M_FRAC
+# what limits each kernel alone on the GPU: "hbm" (streams its arrays), "valu" (vector-instruction
+# issue: valu_issue_frac near 1), "latency" (a chain of dependent steps on few waves)
+KERNEL_BOUND = {
+    "k_tile_hist": "hbm", "k_scatter": "hbm", "k_unit_prep": "hbm", "k_window_rank": "valu", "k_sort_tiles": "lds",
+    "k_rank_tiles": "lds", "k_epoch": "lds", "k_cuts": "hbm", "k_chain_grp8": "valu", "k_chain_grp16": "valu",
+    "k_chain_grp64": "latency", "k_chain_seg": "latency", "k_chain_exits": "latency", "k_chain_mark": "latency",
+    "k_positions": "hbm", "k_deltas": "valu", "k_write_units": "hbm", "k_chunks": "latency", "k_lists": "latency",
+    "k_dec_sections": "hbm", "k_dec_pair_scan": "latency", "k_dec_perm_seg": "valu", "k_dec_perm_grp": "latency",
+    "k_dec_perm_check": "hbm", "k_dec_records": "hbm",
+}
+
+
+def algorithmic_bytes(kernel, n_records, mix):
+    m, p, c = mix.m, mix.pairs, mix.c
     per = {
         "k_tile_hist": 32,
         "k_scatter": 32 + 16 + 4,
@@ -653,11 +682,14 @@ def algorithmic_bytes(kernel, n_records, c):
         "k_chain_grp8": m * (4 + 4 + 4),
         "k_chain_grp16": m * (4 + 4 + 4),
         "k_chain_mark": m * (4 + 1),
-        "k_positions": m * (4 + 1 + 4 + 1.4 + 4 + 1 + 4 + 1.4 + 1.64 * 8) / 2,  # mean of its two launches (rows, columns)
-        "k_deltas": m * (1.3 * 4 + 0.64 * (4 + 4 + 4)),
+        "k_positions": m * (4 + 1 + 4 + (1 + p) + 4 + 1 + 4 + (1 + p) + (1 + p) * 8) / 2,  # mean of its two launches (rows, columns)
+        "k_deltas": m * (2 * p * 4 + p * (4 + 4 + 4)),
         "k_write_units": m * (4 + 4 + 8) + c,
-                "k_dec_sections": 0.3 * c,
-        "k_dec_perm_grp": m * (0.64 * (8 + 16) + 8),
+        "k_dec_sections": 0.3 * c,
+        # the pair sections once (8 B per pair), perm and its inverse once each (4 + 4 B per matched event)
+        "k_dec_perm_seg": m * (p * 8 + 8),
+        "k_dec_perm_grp": m * (p * 8 + 8),
+        "k_dec_pair_scan": m * p * 8,
         "k_dec_records": c + m * (4 + 8 + 8 + 1) + 32,
         "k_chain_exits": m * 4 * 0.4,   # the parents on the paths from each segment's max-level rows to its first row
         "k_cuts": m * (4 + 4),
@@ -665,26 +697,27 @@ def algorithmic_bytes(kernel, n_records, c):
     return None if per is None else per * n_records
 
 
-PMC_TRAFFIC = "profiles/r02/pmc_traffic.json"
+PMC_TRAFFIC = "profiles/r03/pmc_traffic.json"
 
 
 def pmc_traffic():
     """HBM bytes per record of every kernel from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE
     passes (tools/pmc_traffic.py); None if not collected."""
-    for rel in (PMC_TRAFFIC, "profiles/r01/pmc_traffic.json"):
+    for rel in (PMC_TRAFFIC, "profiles/r02/pmc_traffic.json", "profiles/r01/pmc_traffic.json"):
         try:
             d = json.load(open(os.path.join(ROOT, rel)))
             d.setdefault("kernels", {})
+            d["source"] = rel
             return d
         except (OSError, ValueError):
             continue
     return None
 
 
-def pipeline_bytes(c):
+def pipeline_bytes(mix):
     """Algorithmic bytes of the whole path per record: encode reads 32 B/event and writes c;
     decode reads c + 8m of sorted keys and writes 32 B/event."""
-    return 64 + 2 * c + 8 * M_FRAC
+    return 64 + 2 * mix.c + 8 * mix.m
 
 
 if __name__ == "__main__":

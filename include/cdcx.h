@@ -371,6 +371,12 @@ int cdcx_chain_stats(cdcx_ctx* ctx, int64_t* out, int n);
  * out[2] segments that outgrew 64 slots (lane kernel, global-memory leaf list). */
 int cdcx_chain_tiers(cdcx_ctx* ctx, int64_t* out);
 
+/* Totals of the last device encode (what add() / format() / compress() counted over the batch,
+ * rempi_encoder_cdc.cpp:178-272, rempi_clock_delta_compression.cpp:465-672): out[0] records,
+ * out[1] matched events, out[2] unmatched runs, out[3] with_previous entries, out[4] epoch
+ * sources, out[5] (id, delay) pairs, out[6] tables, out[7] chunks. */
+int cdcx_encode_totals(cdcx_ctx* ctx, int64_t* out);
+
 /* Tables that entered each tier of the permutation rebuild (cdc_prepare_decode_indices,
  * rempi_encoder_cdc.cpp:1301-1386) in the last decode: out[0] all tables (pair segments),
  * out[1] tables with a segment that did not finish or did not check out (whole table in a

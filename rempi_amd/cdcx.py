@@ -123,6 +123,7 @@ _SIGNATURES = {
     "cdcx_chain_stats": ([_vp, _i64p, ctypes.c_int], ctypes.c_int),
     "cdcx_chain_tiers": ([_vp, _i64p], ctypes.c_int),
     "cdcx_decode_tiers": ([_vp, _i64p], ctypes.c_int),
+    "cdcx_encode_totals": ([_vp, _i64p], ctypes.c_int),
 }
 
 _lib = None
@@ -451,6 +452,12 @@ class Context:
         out = np.zeros(3, dtype=np.int64)
         self._check(lib().cdcx_chain_tiers(self._c, _ptr(out, ctypes.c_int64)), "chain_tiers")
         return [int(x) for x in out]
+
+    def encode_totals(self) -> dict:
+        """Totals of the last device encode (cdcx_encode_totals)."""
+        out = np.zeros(8, dtype=np.int64)
+        self._check(lib().cdcx_encode_totals(self._c, _ptr(out, ctypes.c_int64)), "encode_totals")
+        return dict(zip(["records", "matched", "runs", "with_next", "sources", "pairs", "tables", "chunks"], out.tolist()))
 
     def decode_tiers(self):
         """Tables entering each permutation-rebuild tier in the last decode (pair segments, whole

@@ -33,7 +33,7 @@ enum KernelId {
   K_SET_DENSE, K_TILE_HIST, K_HIST_SCAN, K_SCATTER, K_RANK_SCAN,
   K_CHUNKS, K_UNITS_LB, K_LISTS, K_UNIT_PREP, K_WINDOW_RANK, K_SORT_TILES, K_RANK_TILES, K_EPOCH, K_CUTS, K_SEG_LIST, K_SEG_SORT, K_CHAIN_G8, K_CHAIN_G16, K_CHAIN_G64, K_CHAIN_SEG, K_CHAIN_EXITS, K_CHAIN_ENTRIES, K_CHAIN_MARK, K_POSITIONS, K_DELTAS,
   K_WRITE_UNITS, K_CHUNK_HEADERS, K_FOOTER_ORDER, K_FOOTER_WRITE, K_WRITE_KEYS,
-  K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_PAIRS, K_DEC_SEG, K_DEC_CHECK, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS, K_DEC_PACK, K_VERIFY,
+  K_DEC_COUNT_CHUNKS, K_DEC_LIST_CHUNKS, K_DEC_UNITS, K_DEC_SECTIONS, K_DEC_PAIRS, K_DEC_SEG, K_DEC_REDO, K_DEC_CHECK, K_DEC_WIN1, K_DEC_WIN4, K_DEC_PERM, K_DEC_RECORDS, K_DEC_PACK, K_VERIFY,
   K_GEN_TILE_SUMS, K_GEN_RANK_SCAN, K_GEN_FRAMES, K_GEN_AKEYS, K_GEN_ARRIVAL, K_GEN_RECORDS,
   K_COUNT
 };
@@ -41,7 +41,7 @@ const char* kKernelNames[K_COUNT] = {
   "k_set_dense", "k_tile_hist", "k_hist_scan", "k_scatter", "k_rank_scan",
   "k_chunks", "k_units_lb", "k_lists", "k_unit_prep", "k_window_rank", "k_sort_tiles", "k_rank_tiles", "k_epoch", "k_cuts", "k_seg_list", "k_seg_sort", "k_chain_grp8", "k_chain_grp16", "k_chain_grp64", "k_chain_seg", "k_chain_exits", "k_chain_entries", "k_chain_mark",
   "k_positions", "k_deltas", "k_write_units", "k_chunk_headers", "k_footer_order", "k_footer_write", "k_write_keys",
-  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_pair_scan", "k_dec_perm_seg", "k_dec_perm_check", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records", "k_dec_pack_tables", "k_verify_roundtrip",
+  "k_dec_count_chunks", "k_dec_list_chunks", "k_dec_units", "k_dec_sections", "k_dec_pair_scan", "k_dec_perm_seg", "k_dec_perm_redo", "k_dec_perm_check", "k_dec_perm_grp", "k_dec_perm_window4", "k_dec_perm_lane", "k_dec_records", "k_dec_pack_tables", "k_verify_roundtrip",
   "k_gen_tile_sums", "k_gen_rank_scan", "k_gen_frames", "k_gen_akeys", "k_gen_arrival", "k_gen_records"};
 
 struct HipError {
@@ -71,9 +71,9 @@ inline int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 constexpr const char* kAliasRecs = "dec_recs"; // decoded records: a buffer of their own (the T-order records keep the
                                               // stream positions that cdcx_verify_roundtrip_device maps them by)
 constexpr const char* kAliasIdd = "mkey";     // pair ids              <- observed-order keys
-constexpr const char* kAliasDld = "seq";      // pair delays           <- edit sequence (the clock-order keys, "skey", are the decoder's input)
+constexpr const char* kAliasDld = "chainbuf"; // pair delays           <- chain / edit-sequence scratch (the clock-order keys, "skey", are the decoder's input)
 constexpr const char* kAliasWpd = "run_cnt";  // with_previous         <- unmatched run counts
-constexpr const char* kAliasUidd = "ep_rank"; // unmatched ids         <- epoch ranks
+constexpr const char* kAliasUidd = "cuts2";   // unmatched ids         <- segment ends / first untaken columns / edit-sequence ids
 constexpr const char* kAliasPerm = "cord";    // perm                  <- clock order of rows
 constexpr const char* kAliasCinv = "inv";     // perm^-1               <- row of each clock
 constexpr const char* kAliasWnf = "chain";    // with_next flags       <- chain flags
@@ -225,6 +225,7 @@ struct cdcx_ctx {
   std::vector<int32_t> map_sets;
   int64_t chain_tier_counts[3] = {0, 0, 0};  // segments entering each tier in the last encode
   int32_t chain_cnt0[4] = {0, 0, 0, 0};      // (host image of the tiers' counters at launch)
+  int64_t enc_totals[8] = {};                // records, matched, runs, with_next, sources, pairs, tables, chunks of the last encode
   int64_t dec_tier_counts[7] = {0, 0, 0, 0, 0, 0, 0};  // tables entering each rebuild tier in the last decode; segments
 
   template <class T>
@@ -235,7 +236,7 @@ struct cdcx_ctx {
       if (b.p) HIPCHK(hipFree(b.p));
       b.p = nullptr;
       b.cap = 0;
-      size_t want = bytes + bytes / 8;
+      size_t want = bytes + bytes / 32;  // (a little room: the ranks of a job differ by a few records)
       if (hipMalloc(&b.p, want) != hipSuccess) {
         (void)hipGetLastError();
         if (hipMalloc(&b.p, bytes) != hipSuccess) {
@@ -546,7 +547,8 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   c->launch(K_LISTS, k_fill_units, dim3(C), dim3(kMaxSets), s, (const Chunk*)d_chunks, (const int64_t*)d_lb_off,
             (const int2*)d_lohi, (const int32_t*)d_nsets, (const int32_t*)d_setlist, (const int64_t*)d_rec_off,
             (const int64_t*)d_cw1, d_units, d_w1);
-  uint64_t* d_mkey = c->buf<uint64_t>("mkey", N);
+  // (one more word per table: the lane tier's leaf lists and the chain exits live here once the ranks are known)
+  uint64_t* d_mkey = c->buf<uint64_t>("mkey", (size_t)(N + lbn));
   int32_t* d_midx = c->buf<int32_t>("midx", N);
   int32_t* d_wp = c->buf<int32_t>("wp", N);
   int32_t* d_run_id = c->buf<int32_t>("run_id", N);
@@ -572,10 +574,20 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     c->launch(K_WINDOW_RANK, k_window_rank_wide, dim3((unsigned)lbn), dim3(256), s, d_units, (const uint64_t*)d_mkey, d_cord,
               d_inv, d_skey);
   }
-  uint64_t* d_ep_rank = c->buf<uint64_t>("ep_rank", N);
-  uint64_t* d_ep_clk = c->buf<uint64_t>("ep_clk", N);
-  int32_t* d_segend = c->buf<int32_t>("segend", N);
-  int32_t* d_opn = c->buf<int32_t>("opn", N);  // column + open flag of every row (k_cuts)
+  // Epoch lines: kMaxUnitSources entries per table when that is less than one per record
+  // (few large tables, the usual case), else at the table's T-order start.
+  const int64_t ep_stride = (lbn * (int64_t)kMaxUnitSources < N) ? kMaxUnitSources : 0;
+  const size_t ep_n = ep_stride ? (size_t)(lbn * ep_stride) : (size_t)N;
+  uint64_t* d_ep_rank = c->buf<uint64_t>("ep_rank", ep_n);
+  uint64_t* d_ep_clk = c->buf<uint64_t>("ep_clk", ep_n);
+  // Scratch of the chain and the edit sequence, reused as the phases follow each other:
+  //   cuts2    [segend | opn]            (k_cuts -> k_seg_list / the chain tiers), then sx (k_pos_cols -> k_deltas)
+  //   chainbuf [par | exta | topg | qn]  (chain tiers -> exits, entries, mark), then [posA | crow | seq] (positions -> deltas)
+  //   mkey     observed-order keys       (k_unit_prep -> rank), then the lane tier's leaf lists, then qexit (exits -> entries)
+  const size_t Np = (size_t)(N + lbn + 63) / 64 * 64;
+  int32_t* d_cuts2 = c->buf<int32_t>("cuts2", 2 * Np);
+  int32_t* d_segend = d_cuts2;
+  int32_t* d_opn = d_cuts2 + Np;  // column + open flag of every row (k_cuts)
   int64_t* d_bound = c->buf<int64_t>("fbound", R);
   EncTotals tot{};
   std::vector<int64_t> bound(R, 0);
@@ -591,7 +603,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     memcpy(bound.data(), h + o_b, 8 * (size_t)R);
   };
   auto epoch_cuts = [&](unsigned grid) {
-    c->launch(K_EPOCH, k_epoch<512>, dim3(grid), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, d_err);
+    c->launch(K_EPOCH, k_epoch<512>, dim3(grid), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, ep_stride, d_err);
     // Chain: closed-prefix segments simulated independently, then stitched (chain.hip).
     c->launch(K_CUTS, k_cuts, dim3(grid), dim3(256), s, d_units, (const int32_t*)d_inv, d_segend, d_opn);
     totals();
@@ -616,14 +628,14 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
               (const uint64_t*)d_tmm, d_cord, d_inv, d_skey);
     for (Unit& u : units) u.wfail = u.wfail ? 0 : 2;  // epoch and cuts for the re-ranked units only
     d_units = c->upload("units", units, s);
-    c->launch(K_EPOCH, k_epoch<512>, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, d_err);
+    c->launch(K_EPOCH, k_epoch<512>, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank, d_ep_clk, ep_stride, d_err);
     c->launch(K_CUTS, k_cuts, dim3(NU), dim3(256), s, d_units, (const int32_t*)d_inv, d_segend, d_opn);
     c->launch(K_LISTS, k_units_clear_wfail, dim3(blocks(NU, 256)), dim3(256), s, d_units, NU);
     totals();
   }
   if (tot.n_big > 0) {  // > 256 sources in some table
     c->launch(K_EPOCH, k_epoch<2 * kMaxUnitSources>, dim3(NU), dim3(256), s, d_units, (const uint64_t*)d_skey, d_ep_rank,
-              d_ep_clk, d_err);
+              d_ep_clk, ep_stride, d_err);
     totals();
   }
   const int64_t nsegs = tot.n_segs;
@@ -645,7 +657,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int32_t* d_fbucket = c->buf<int32_t>("fbucket", fb_off[R]);
   int32_t* d_fcount = c->buf<int32_t>("fcount", R);
   c->launch(K_FOOTER_ORDER, k_footer_order, dim3(R), dim3(256), s, (const Unit*)d_units,
-            (const int32_t*)d_ufirst, (const int32_t*)d_nunits, (const uint64_t*)d_ep_rank, R, (const int64_t*)d_fk_off,
+            (const int32_t*)d_ufirst, (const int32_t*)d_nunits, (const uint64_t*)d_ep_rank, ep_stride, R, (const int64_t*)d_fk_off,
             (const int64_t*)d_fb_off, d_fkey, d_fnext, d_fbucket, d_fcount);
 
   // Output layout on the device: as soon as the pair counts are known (after the chain), so
@@ -658,7 +670,7 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   int2* d_keys = reinterpret_cast<int2*>(d_skey);
   int64_t* d_upre = c->buf<int64_t>("upre", (size_t)NU + 1);
   int64_t* d_cpre = c->buf<int64_t>("cpre", (size_t)C + 1);
-  int64_t* d_files = c->buf<int64_t>("file_layout", 3 * (size_t)R + 1);  // file_off[R], file_len[R], foot_off[R], total
+  int64_t* d_files = c->buf<int64_t>("file_layout", 3 * (size_t)R + 2);  // file_off[R], file_len[R], foot_off[R], total, table bytes
   auto out_layout = [&] {
     c->launch(K_LISTS, k_out_layout, dim3(1), dim3(kScanBlock), s, d_units, d_chunks, C, (const int32_t*)d_cbase, R,
               (const int32_t*)d_fcount, (int32_t)c->rep, (const EncTotals*)d_tot, d_upre, d_cpre, d_files, d_files + R,
@@ -675,16 +687,15 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   c->launch(K_SEG_SORT, k_seg_bins, dim3(1), dim3(256), s, d_seghist);
   c->launch(K_SEG_SORT, k_seg_order, dim3(blocks(nsegs, 1024)), dim3(256), s, (const Seg*)d_segs, (int32_t)nsegs, d_seghist,
             d_segord);
-  int32_t* d_par = c->buf<int32_t>("par", N);
-  int32_t* d_exta = c->buf<int32_t>("exta", N);
-  int32_t* d_topg = c->buf<int32_t>("topg", N);
-  int32_t* d_qn = c->buf<int32_t>("qn", N);
+  int32_t* d_chainbuf = c->buf<int32_t>("chainbuf", 4 * Np);
+  int32_t* d_par = d_chainbuf;
+  int32_t* d_exta = d_chainbuf + Np;
+  int32_t* d_topg = d_chainbuf + 2 * Np;
+  int32_t* d_qn = d_chainbuf + 3 * Np;
   uint8_t* d_chain = c->buf<uint8_t>("chain", N);  // every row written by k_chain_mark
   // Tiers: 8-lane groups with 16 leaf slots; segments whose leaf list outgrows them go to
   // 64-lane groups, then to the lane kernel's exact global-memory path.  Each tier rewrites
   // every output of the segments it takes.
-  // (two words per record and unit: the edit sequence later, the lane tier's leaf lists before that)
-  uint32_t* d_seq = c->buf<uint32_t>("seq", 2 * (size_t)(N + lbn));
   int32_t* d_cnt = c->buf<int32_t>("chain_cnt", 4);
   int32_t* d_ovf1 = c->buf<int32_t>("chain_ovf1", nsegs);
   int32_t* d_ovf2 = c->buf<int32_t>("chain_ovf2", nsegs);
@@ -719,15 +730,15 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
       list = d_ovf2;
       nlist = d_cnt + 2;
     }
-    // The lane tier's exact leaf lists live in the edit sequence's buffer, which is written later.
-    int2* d_leaves = reinterpret_cast<int2*>(d_seq);
+    // The lane tier's exact leaf lists live where the observed-order keys were (the ranks are known).
+    int2* d_leaves = reinterpret_cast<int2*>(d_mkey);
     c->launch(K_CHAIN_SEG, k_chain_seg<16>,
               dim3((unsigned)(c->chain_tier >= 2 ? std::max<int64_t>(1, std::min<int64_t>(1024, blocks(nsegs, 256))) : 16)),
               dim3(256), s, (const Unit*)d_units, d_segs, nlist, list, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par,
               d_exta, d_topg, d_qn, d_leaves, (const int64_t*)d_w1, d_err,
               c->chain_stats ? c->buf<unsigned long long>("chain_stats", 8) : (unsigned long long*)nullptr);
   }
-  int32_t* d_qexit = c->buf<int32_t>("qexit", N);
+  int32_t* d_qexit = reinterpret_cast<int32_t*>(d_mkey);  // (the leaf lists are done with)
   c->launch(K_CHAIN_EXITS, k_chain_exits, dim3((unsigned)std::min<int64_t>(8192, blocks(nsegs, 256))), dim3(256), s,
             (const Unit*)d_units, (const Seg*)d_segs, (int32_t)nsegs, (const int32_t*)d_par, (const int32_t*)d_exta,
             (const int32_t*)d_qn, d_qexit, d_err);
@@ -736,9 +747,11 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   c->launch(K_CHAIN_MARK, k_chain_mark, dim3((unsigned)std::min<int64_t>(8192, blocks(nsegs, 4))), dim3(256), s, (const Unit*)d_units,
             (const Seg*)d_segs, (int32_t)nsegs, (const int32_t*)d_par, (const int32_t*)d_qn, d_chain);
   out_layout();  // (the pair counts are final: k_chain_entries)
-  int32_t* d_posA = c->buf<int32_t>("posA", N);
-  int32_t* d_crow = c->buf<int32_t>("crow", N);
-  int32_t* d_sx = c->buf<int32_t>("sx", 2 * N);
+  // (par, exta, topg, qn, segend and opn are done with: k_chain_mark was their last reader)
+  int32_t* d_posA = d_chainbuf;
+  int32_t* d_crow = d_chainbuf + Np;
+  uint32_t* d_seq = reinterpret_cast<uint32_t*>(d_chainbuf + 2 * Np);
+  int32_t* d_sx = d_cuts2;
   c->launch_gated(2, NU >= 4096 && (c->gate_bw & 16), K_POSITIONS, k_pos_rows, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_cord,
             (const uint8_t*)d_chain, d_posA, d_crow);
   c->launch_gated(2, NU >= 4096 && (c->gate_bw & 16), K_POSITIONS, k_pos_cols, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_inv,
@@ -750,14 +763,14 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
   if (c->rep) out_layout();
   c->launch_gated(2, NU >= 4096 && (c->gate_bw & 32), K_WRITE_UNITS, k_write_units, dim3(NU), dim3(256), s, (const Unit*)d_units, (const int32_t*)d_midx,
             (const int32_t*)d_wp, (const int32_t*)d_run_id, (const uint64_t*)d_run_cnt, (const uint64_t*)d_ep_rank,
-            (const uint64_t*)d_ep_clk, (int32_t)c->rep, d_out);
+            (const uint64_t*)d_ep_clk, ep_stride, (int32_t)c->rep, d_out);
   c->launch(K_CHUNK_HEADERS, k_chunk_headers, dim3(blocks(C, 256)), dim3(256), s, (const Chunk*)d_chunks, C, d_out);
   c->launch(K_FOOTER_WRITE, k_footer_write, dim3(blocks(R, 64)), dim3(64), s, (const int64_t*)d_fk_off,
             (const int64_t*)d_fb_off, (const uint64_t*)d_fkey, (const int32_t*)d_fnext, (const int32_t*)d_fbucket,
             (const int32_t*)d_fcount, (const int64_t*)(d_files + 2 * R), R, d_out);
   {  // wait 3: error word, file offsets and lengths, the chain tiers' counts
-    Mail m(c, s, 128 + 8 * (3 * (size_t)R + 1));
-    const size_t o_err = m.add(d_err, 4), o_f = m.add(d_files, 8 * (3 * (size_t)R + 1));
+    Mail m(c, s, 128 + 8 * (3 * (size_t)R + 2));
+    const size_t o_err = m.add(d_err, 4), o_f = m.add(d_files, 8 * (3 * (size_t)R + 2));
     const size_t o_cnt = m.add(c->rep ? (const void*)d_err : (const void*)c->buf<int32_t>("chain_cnt", 4), c->rep ? 4 : 12);
     const uint8_t* h = m.wait();
     raise_device_error(*reinterpret_cast<const uint32_t*>(h + o_err));
@@ -771,6 +784,9 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
     file_off.assign(f, f + R);
     file_len.assign(f + R, f + 2 * R);
     if (f[3 * R] > total_max) throw CdcxError{CDCX_ERR_CORRUPT, "output layout exceeds its bound"};
+    const int64_t fixed = 72ll * NU + 16ll * tot.sources + (c->rep ? 0 : 8ll * tot.with_next + 8ll * tot.matched + 16ll * tot.runs);
+    const int64_t totals[8] = {N, tot.matched, tot.runs, tot.with_next, tot.sources, c->rep ? 0 : (f[3 * R + 1] - fixed) / 8, NU, C};
+    std::copy(totals, totals + 8, c->enc_totals);
   }
   c->d_out = d_out;
   c->d_keys = d_keys;
@@ -897,7 +913,7 @@ void decode_batch(cdcx_ctx* c, int32_t R, const uint8_t* d_in, const std::vector
       c->launch(K_DEC_CHECK, k_dec_perm_check, dim3(blocks(nsegs, 8)), dim3(256), s, d_units, (const DSeg*)d_segs, nsegs,
                 (const int32_t*)d_dump_t, (const int32_t*)d_dump_w, list, kRedoCap, d_redone, d_nfail);
       if (list)
-        c->launch(K_DEC_SEG, k_dec_perm_seg<2>, dim3(kRedoCap / 4), dim3(64), s, d_units, (const int32_t*)list,
+        c->launch(K_DEC_REDO, k_dec_perm_seg<2>, dim3(kRedoCap / 4), dim3(64), s, d_units, (const int32_t*)list,
                   (const DSeg*)d_segs, (int64_t)kRedoCap, 0, d_in, (const int64_t*)d_pcar, d_perm, d_cinv, d_dump_t,
                   d_dump_w, d_nfail);
     }
@@ -2187,6 +2203,12 @@ int cdcx_kernel_times(cdcx_ctx* c, double* ms, int64_t* launches, int n) {
 int cdcx_chain_tiers(cdcx_ctx* c, int64_t* out) {
   if (!c || !out) return CDCX_ERR_ARG;
   for (int k = 0; k < 3; k++) out[k] = c->chain_tier_counts[k];
+  return CDCX_OK;
+}
+
+int cdcx_encode_totals(cdcx_ctx* c, int64_t* out) {
+  if (!c || !out) return CDCX_ERR_ARG;
+  std::copy(c->enc_totals, c->enc_totals + 8, out);
   return CDCX_OK;
 }
 

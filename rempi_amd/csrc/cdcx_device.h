@@ -100,6 +100,14 @@ __device__ __host__ __forceinline__ uint64_t key_words(uint64_t k) { return k ^ 
 
 __device__ __forceinline__ uint64_t sext(int32_t v) { return (uint64_t)(int64_t)v; }
 
+// Where a unit's epoch line (sources and their last clocks, at most kMaxUnitSources entries)
+// sits in the epoch scratch arrays: kMaxUnitSources entries per unit when the batch's units are
+// few and large (stride != 0), else at the unit's T-order start (a unit has at least as many
+// records as sources).
+__device__ __forceinline__ int64_t epoch_slot(int64_t unit, int64_t a, int64_t stride) {
+  return stride ? unit * stride : a;
+}
+
 // Unaligned-safe 8-byte little-endian store into the byte output (all CDC sections are
 // 8-byte multiples and every unit starts 8-aligned, so these are aligned in practice).
 __device__ __forceinline__ void st_u64(uint8_t* p, uint64_t v) { *reinterpret_cast<uint64_t*>(p) = v; }

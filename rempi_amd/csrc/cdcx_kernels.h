@@ -40,7 +40,7 @@ __global__ void k_sort_tiles(const Unit*, const SortTile*, const uint64_t*, uint
 __global__ void k_rank_tiles(const Unit*, const SortTile*, const uint64_t*, const uint64_t*, const int32_t*,
                              const uint64_t*, int32_t*, int32_t*, uint64_t*);
 template <int HCAP>
-__global__ void k_epoch(Unit*, const uint64_t*, uint64_t*, uint64_t*, uint32_t*);
+__global__ void k_epoch(Unit*, const uint64_t*, uint64_t*, uint64_t*, int64_t, uint32_t*);
 // chain.hip
 __global__ void k_cuts(Unit*, const int32_t*, int32_t*, int32_t*);
 __global__ void k_seg_list(const Unit*, const int32_t*, Seg*);
@@ -65,9 +65,9 @@ __global__ void k_pos_cols(const Unit*, const int32_t*, const uint8_t*, const in
                            int32_t*);
 __global__ void k_deltas(const Unit*, const uint32_t*, const int32_t*, uint8_t*);
 __global__ void k_write_units(const Unit*, const int32_t*, const int32_t*, const int32_t*, const uint64_t*,
-                              const uint64_t*, const uint64_t*, int32_t, uint8_t*);
+                              const uint64_t*, const uint64_t*, int64_t, int32_t, uint8_t*);
 __global__ void k_chunk_headers(const Chunk*, int32_t, uint8_t*);
-__global__ void k_footer_order(const Unit*, const int32_t*, const int32_t*, const uint64_t*, int32_t, const int64_t*,
+__global__ void k_footer_order(const Unit*, const int32_t*, const int32_t*, const uint64_t*, int64_t, int32_t, const int64_t*,
                                const int64_t*, uint64_t*, int32_t*, int32_t*, int32_t*);
 __global__ void k_footer_write(const int64_t*, const int64_t*, const uint64_t*, const int32_t*, const int32_t*,
                                const int32_t*, const int64_t*, int32_t, uint8_t*);

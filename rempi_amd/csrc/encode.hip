@@ -830,7 +830,7 @@ __global__ void __launch_bounds__(256) k_rank_tiles(const Unit* __restrict__ uni
 template <int HCAP>
 __global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const uint64_t* __restrict__ skey,
                                                uint64_t* __restrict__ ep_rank, uint64_t* __restrict__ ep_clk,
-                                               uint32_t* err) {
+                                               int64_t ep_stride, uint32_t* err) {
   constexpr int LCAP = HCAP / 2;  // distinct sources this instance can list
   constexpr bool kBig = HCAP >= 2 * kMaxUnitSources;
   __shared__ int32_t hsrc[HCAP];
@@ -842,6 +842,7 @@ __global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const u
   if (u.wfail != 0) return;  // not ranked yet (k_window_rank), or already done
   if (kBig && u.S != -1) return;
   const int64_t a = u.a, ka = u.key_off;
+  const int64_t ea = epoch_slot(blockIdx.x, a, ep_stride);
   const int32_t M = u.M;
   for (int i = threadIdx.x; i < HCAP; i += 256) {
     hsrc[i] = INT32_MIN;
@@ -923,15 +924,15 @@ __global__ void __launch_bounds__(256) k_epoch(Unit* __restrict__ units, const u
     for (int q = 0; q < S; q++) ho.insert_new((uint64_t)(int64_t)lsrc[q]);
     int j = 0;
     for (int32_t p = ho.head; p != -1; p = ho.next[p], j++) {
-      ep_rank[a + j] = (uint64_t)(int64_t)lsrc[p];
-      ep_clk[a + j] = (uint64_t)(int64_t)lclk[p];
+      ep_rank[ea + j] = (uint64_t)(int64_t)lsrc[p];
+      ep_clk[ea + j] = (uint64_t)(int64_t)lclk[p];
     }
     u.S = S;
   }
 }
 
-template __global__ void k_epoch<512>(Unit*, const uint64_t*, uint64_t*, uint64_t*, uint32_t*);
-template __global__ void k_epoch<2 * kMaxUnitSources>(Unit*, const uint64_t*, uint64_t*, uint64_t*, uint32_t*);
+template __global__ void k_epoch<512>(Unit*, const uint64_t*, uint64_t*, uint64_t*, int64_t, uint32_t*);
+template __global__ void k_epoch<2 * kMaxUnitSources>(Unit*, const uint64_t*, uint64_t*, uint64_t*, int64_t, uint32_t*);
 
 // ---------------------------------------------------------------------------------------
 // Edit-sequence positions (A8).  With chain rows r_1<..<r_K (columns col_k) and r_0 =
@@ -1263,10 +1264,11 @@ __global__ void __launch_bounds__(256) k_write_units(const Unit* __restrict__ un
                                                      const int32_t* __restrict__ wp, const int32_t* __restrict__ run_id,
                                                      const uint64_t* __restrict__ run_cnt,
                                                      const uint64_t* __restrict__ ep_rank,
-                                                     const uint64_t* __restrict__ ep_clk, int32_t rep,
+                                                     const uint64_t* __restrict__ ep_clk, int64_t ep_stride, int32_t rep,
                                                      uint8_t* __restrict__ out) {
   Unit u = units[blockIdx.x];
   const int64_t a = u.a;
+  const int64_t ea = epoch_slot(blockIdx.x, a, ep_stride);
   uint8_t* o = out + u.out_off;
   const int t = threadIdx.x;
   // REMPI_ENCODE=7 (rempi_encoder_rep.cpp:50-146): the same table with every section after
@@ -1280,8 +1282,8 @@ __global__ void __launch_bounds__(256) k_write_units(const Unit* __restrict__ un
   }
   uint8_t* p = o + 16;
   for (int i = t; i < u.S; i += 256) {
-    st_u64(p + 8 * i, ep_rank[a + i]);
-    st_u64(p + 8 * (u.S + i), ep_clk[a + i]);
+    st_u64(p + 8 * i, ep_rank[ea + i]);
+    st_u64(p + 8 * (u.S + i), ep_clk[ea + i]);
   }
   p += 16ull * u.S;
   if (t == 0) {
@@ -1324,7 +1326,7 @@ __global__ void __launch_bounds__(256) k_chunk_headers(const Chunk* __restrict__
 // holds replays every insertion sequentially.
 __global__ void __launch_bounds__(256) k_footer_order(const Unit* __restrict__ units, const int32_t* __restrict__ ufirst,
                                                       const int32_t* __restrict__ nunits, const uint64_t* __restrict__ ep_rank,
-                                                      int32_t n_ranks, const int64_t* __restrict__ fk_off,
+                                                      int64_t ep_stride, int32_t n_ranks, const int64_t* __restrict__ fk_off,
                                                       const int64_t* __restrict__ fb_off, uint64_t* __restrict__ fkey,
                                                       int32_t* __restrict__ fnext, int32_t* __restrict__ fbucket,
                                                       int32_t* __restrict__ fcount) {
@@ -1346,7 +1348,7 @@ __global__ void __launch_bounds__(256) k_footer_order(const Unit* __restrict__ u
   for (int32_t q = w; q < nu; q += 4) {
     const Unit u = units[u0 + q];
     for (int32_t j = l; j < u.S; j += 64) {
-      const int32_t k = (int32_t)ep_rank[u.a + j];
+      const int32_t k = (int32_t)ep_rank[epoch_slot(u0 + q, u.a, ep_stride) + j];
       const unsigned long long ord = ((unsigned long long)q << 12) | (unsigned long long)j;
       uint32_t h = ((uint32_t)k * 2654435761u) % HC;
       for (int probe = 0; probe < HC; probe++) {
@@ -1369,7 +1371,7 @@ __global__ void __launch_bounds__(256) k_footer_order(const Unit* __restrict__ u
       for (int32_t q = 0; q < nu; q++) {
         const Unit u = units[u0 + q];
         for (int32_t j = 0; j < u.S; j++) {
-          const uint64_t k = (uint64_t)(int64_t)(int32_t)ep_rank[u.a + j];
+          const uint64_t k = (uint64_t)(int64_t)(int32_t)ep_rank[epoch_slot(u0 + q, u.a, ep_stride) + j];
           if (!ho.contains(k)) ho.insert_new(k);
         }
       }

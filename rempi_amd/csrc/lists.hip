@@ -244,7 +244,10 @@ __global__ void __launch_bounds__(kScanBlock) k_out_layout(Unit* __restrict__ un
       foot_off[r] = ex + fsz - (20 + 4ll * fcount[r]);
     }
   }
-  if (threadIdx.x == 0) *total = carry;
+  if (threadIdx.x == 0) {
+    total[0] = carry;
+    total[1] = upre[NU];  // bytes of all tables (the host reads the number of pairs off it)
+  }
   __syncthreads();
   for (int32_t c = threadIdx.x; c < C; c += kScanBlock) {
     Chunk& ch = chunks[c];
