@@ -515,6 +515,10 @@ def main():
         [n_records * args.steps, comp_bytes, ver["enc_ranks"], ver["enc_fail"], ver["dec_ranks"], ver["dec_fail"],
          count if args.max_batches <= 0 else sum(n for _, n in plan), n_records, n_matched, n_pairs], elapsed, dist,
         "cuda" if backend == "nccl" else "cpu")
+    if dist:  # the last collective is done: what follows (CPU baseline, config 2, the JSON line) is rank 0's alone
+        dist.barrier()
+        dist.destroy_process_group()
+        dist = None
     total_records = counters[0]
     value = total_records * RECORD_BYTES / tmax / 1e9
     comp_per_event = counters[1] / max(total_records, 1)

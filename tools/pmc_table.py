@@ -16,7 +16,9 @@ disp = collections.defaultdict(set)
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("cdcx::", "")
-        k = {"k_chain_grp<16>": "k_chain_grp16", "k_chain_grp<64>": "k_chain_grp64", "k_epoch<512>": "k_epoch"}.get(k, k)
+        k = {"k_chain_grp<16>": "k_chain_grp16", "k_chain_grp<64>": "k_chain_grp64", "k_epoch<512>": "k_epoch",
+             "k_dec_perm_seg<0>": "k_dec_perm_grp", "k_dec_perm_seg<1>": "k_dec_perm_seg", "k_dec_perm_seg<2>": "k_dec_perm_redo",
+             "k_chain_seg<16>": "k_chain_seg"}.get(k, k)
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r["Dispatch_Id"])
 recs = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0
