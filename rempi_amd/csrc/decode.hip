@@ -572,7 +572,11 @@ __global__ void __launch_bounds__(64) k_dec_pair_scan(const DUnit* __restrict__ 
 // check out).
 //
 // The list is held as a window of list positions [base, base + W) in a per-group LDS ring,
-// plus an LDS map element -> position for the elements in the window.  Every position at
+// plus an LDS map from an element's low bits to the ring slot it was last put in (one byte
+// per entry: the LDS a group needs decides how many groups a CU holds, and the rebuild is
+// bound by the latency of its dependent steps, not by issue).  An entry is a hint: the slot's
+// content says whether the element is there, so stale and colliding entries cost a failed
+// look-up (the unit goes to the next tier), never a wrong move.  Every position at
 // or past the window still holds its initial element (position q holds q): nothing has
 // been moved there.  A pair moves x from its position p to t = p + delay of the list
 // without x, i.e. rotates the window slots between p and t by one: one LDS read + write
@@ -627,8 +631,20 @@ __device__ __forceinline__ int64_t row_incl_scan64(int64_t v) {  // inclusive sc
 
 template <int Q>
 __device__ __forceinline__ int32_t row_bcast(int32_t v) {
-  return __builtin_amdgcn_update_dpp(0, v, 0x150 + Q, 0xf, 0xf, false);  // row_newbcast:Q
+  // row_newbcast:Q (every lane has a source: bound_ctrl only spares the copy of an old value)
+  return __builtin_amdgcn_update_dpp(0, v, 0x150 + Q, 0xf, 0xf, true);
 }
+
+// Lane masks of a compare, straight from v_cmp into a scalar register pair (LLVM integer
+// predicates), and a lane's own bit of such a mask as a select condition.
+using mask64 = unsigned long long;
+__device__ __forceinline__ mask64 m_lt(int32_t x, int32_t y) { return __builtin_amdgcn_sicmp(x, y, 40); }
+__device__ __forceinline__ mask64 m_le(int32_t x, int32_t y) { return __builtin_amdgcn_sicmp(x, y, 41); }
+__device__ __forceinline__ mask64 m_gt(int32_t x, int32_t y) { return __builtin_amdgcn_sicmp(x, y, 38); }
+__device__ __forceinline__ mask64 m_ge(int32_t x, int32_t y) { return __builtin_amdgcn_sicmp(x, y, 39); }
+__device__ __forceinline__ mask64 m_ne(int32_t x, int32_t y) { return __builtin_amdgcn_sicmp(x, y, 33); }
+__device__ __forceinline__ mask64 mu_ge(uint32_t x, uint32_t y) { return __builtin_amdgcn_uicmp(x, y, 35); }
+__device__ __forceinline__ bool lane_of(mask64 m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 }  // namespace
 
 template <int MODE>  // 0: whole units (`order`), 1: all segments, 2: the segments listed in `order` again, from dumpT
@@ -640,10 +656,10 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
                                                      int32_t* __restrict__ nfail) {
   constexpr int32_t W = kGW, WM = kGW - 1, MM = kGMap - 1;
   __shared__ int32_t win_all[4][W + 16];      // + one dummy slot per lane
-  __shared__ int2 emap_all[4][kGMap + 16];    // {element, absolute position}; + dummies
+  __shared__ uint8_t emap_all[4][kGMap + 16];  // ring slot of the element with these low bits; + dummies
   const int g = threadIdx.x >> 4, j = threadIdx.x & 15;
   int32_t* win = win_all[g];
-  int2* emap = emap_all[g];
+  uint8_t* emap = emap_all[g];
   constexpr bool SEG = MODE != 0, REDO = MODE == 2;
   int64_t gi = (int64_t)blockIdx.x * 4 + g;
   int32_t ui = -1;
@@ -677,6 +693,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
     if (!SEG) sd.ke = Pu;
   }
   const bool wact = SEG && sim && sd.s > 0;            // replays kSegWarm pairs first
+  const mask64 wactm = __builtin_amdgcn_ballot_w64(wact);
   const bool hasn = SEG && sd.cap != kSegNoCap;        // a segment follows: leave it the final state
   const int32_t ka = sd.ka, ke = sim ? sd.ke : sd.ka;  // the group's own pairs
   const int32_t klo = wact ? ka - kSegWarm : ka;       // first pair it reads
@@ -694,15 +711,18 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
     cxd = o[3];
   }
   int32_t base = sd.base0;  // (a multiple of 16)
-  for (int32_t q = j; q < kGMap; q += 16) emap[q] = make_int2(-1, -1);
-  for (int32_t q = j; q < W; q += 16) {  // (entries of lane j only: in program order with the loop above)
+  for (int32_t q = j; q < W; q += 16) {  // (map entries of elements outside the window: never trusted, see step)
     const int32_t e = base + q;
     win[e & WM] = e;
-    emap[e & MM] = make_int2(e, e);
+    emap[e & MM] = (uint8_t)(e & WM);
   }
-  int32_t failv = sim ? 0 : 1;
-  auto slide = [&](auto warm_c, bool go) {  // settle [base, base+16), open [base+W, base+W+16) as identity
+  // Flags of a step are wave-uniform lane masks in scalar registers (group-uniform conditions
+  // set all 16 bits of a group): combining and testing them is scalar work, and a lane reads
+  // its bit straight from the mask as a select operand.
+  mask64 failm = ~__builtin_amdgcn_ballot_w64(sim);  // groups that take no (more) pairs at this tier
+  auto slide = [&](auto warm_c, mask64 gom) {  // settle [base, base+16), open [base+W, base+W+16) as identity
     constexpr bool WARM = decltype(warm_c)::value;
+    const bool go = lane_of(gom);
     const int32_t ph = go ? ((base + j) & WM) : W + j;
     const int32_t v = win[ph];  // (dummy slot when not sliding)
     if (!WARM) {
@@ -714,43 +734,59 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
     const int32_t e = base + W + j;
     __builtin_amdgcn_wave_barrier();
     win[ph] = e;
-    emap[go ? (e & MM) : kGMap + j] = make_int2(e, e);
-    if (go) base += 16;
+    emap[go ? (e & MM) : kGMap + j] = (uint8_t)ph;  // (e's ring slot is the one just settled)
+    base += go ? 16 : 0;
   };
   // one pair of all four groups: x, d group-uniform.  WARM: the replay before a segment's own
   // pairs -- the window stays at or below `own`, nothing is written, and a pair that does not
   // fit is skipped (the state is checked afterwards).  Otherwise the window stays at or below
   // `cap` and a pair that does not fit fails the unit.
-  auto step = [&](auto warm_c, bool in_range, int32_t x, int32_t d) {
+  auto step = [&](auto warm_c, mask64 in_m, int32_t x, int32_t d) {
       constexpr bool WARM = decltype(warm_c)::value;
       const int32_t lim = WARM ? own : cap;
       // Common path without divergent branches: predicated selects, LDS accesses of
       // inactive lanes go to per-lane dummy slots; rare cases (slides, targets past the
       // window, rotations longer than 16 slots) take wave-uniform detours.
       // (an id outside [0, M) has failed the unit when its batch was formed, in lp())
-      // (flags of one step are lane masks; only the unit's failure is carried as a word)
-      bool act = in_range & (failv == 0);
+      mask64 actm = in_m & ~failm;
       // an untouched x (at position x) is brought kGAhead slots before the window end
-      const bool far = act & (x >= base + W);
-      if (__builtin_amdgcn_ballot_w64(far))
-        while (__builtin_amdgcn_ballot_w64(far && x >= base + W - kGAhead && base + 16 <= lim))
-          slide(warm_c, far && x >= base + W - kGAhead && base + 16 <= lim);
-      const int2 e = emap[act ? (x & MM) : kGMap + j];
-      int32_t p = e.y - base;
+      const mask64 farm = actm & m_ge(x, base + W);
+      if (farm)
+        while (true) {
+          const mask64 gom = farm & m_ge(x, base + W - kGAhead) & m_le(base + 16, lim);
+          if (!gom) break;
+          slide(warm_c, gom);
+        }
+      // the map gives a ring slot; x is there or the entry is stale (another element with the
+      // same low bits, or none): the slot's content decides, read beside the rotation's first
+      // read below, so that the check costs no LDS round trip of its own
+      const int32_t slot = emap[lane_of(actm) ? (x & MM) : kGMap + j] & WM;
+      int32_t p = (slot - base) & WM;
       int32_t t = p + d;
-      const bool bad = act & ((e.x != x) | ((uint32_t)p >= (uint32_t)W) | (t < 0) | (base + t > M - 1));
-      if (!WARM) failv |= bad ? 1 : 0;
-      act &= !bad;
-      if (__builtin_amdgcn_ballot_w64(act && t > W - 1)) {
-        while (__builtin_amdgcn_ballot_w64(act && t > W - 1)) {
-          const bool go = act & (t > W - 1);
-          const bool stuck = go & ((p < 16) | (base + 16 > lim));
-          if (!WARM) failv |= stuck ? 1 : 0;
-          act &= !stuck;
-          const bool sl = go & !stuck;
-          slide(warm_c, sl);
-          p -= sl ? 16 : 0;
-          t -= sl ? 16 : 0;
+      const mask64 badm = actm & (m_lt(t, 0) | m_gt(base + t, M - 1));
+      if (!WARM) failm |= badm;
+      actm &= ~badm;
+      auto in_slot = [&]() {  // drops the groups whose x is not in `slot`
+        int32_t chk = win[lane_of(actm) ? slot : W + j];
+        asm volatile("" : "+v"(chk));
+        const mask64 missm = actm & m_ne(chk, x);
+        if (!WARM) failm |= missm;
+        actm &= ~missm;
+      };
+      mask64 overm = actm & m_gt(t, W - 1);
+      if (overm) {
+        in_slot();  // (before the window moves on account of x)
+        overm &= actm;
+        while (overm) {
+          const mask64 stuckm = overm & (m_lt(p, 16) | m_gt(base + 16, lim));
+          if (!WARM) failm |= stuckm;
+          actm &= ~stuckm;
+          const mask64 slm = overm & ~stuckm;
+          slide(warm_c, slm);
+          const int32_t back = lane_of(slm) ? 16 : 0;
+          p -= back;
+          t -= back;
+          overm = actm & m_gt(t, W - 1);
         }
       }
       // rotation of the slots between p and t, 16 at a time
@@ -759,20 +795,23 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
       const int32_t dir = fwd ? 1 : -1;
       auto chunk = [&](int32_t c) {
         const int32_t o = c + j;
-        const bool sel = act && o <= len;
+        const mask64 ltm = m_lt(o, len);
         const int32_t s = p + dir * o;
-        const int32_t rd = (sel && o < len) ? ((base + s + dir) & WM) : W + j;
+        const int32_t rd = lane_of(actm & ltm) ? ((base + s + dir) & WM) : W + j;
         int32_t w = win[rd];
         asm volatile("" : "+v"(w));  // keep the read unconditional (no exec-mask branch around it)
-        const int32_t v = (o < len) ? w : x;
+        if (c == 0) in_slot();
+        const bool sel = lane_of(actm & m_le(o, len));
+        const int32_t v = lane_of(ltm) ? w : x;
+        const int32_t ws = (base + s) & WM;
         __builtin_amdgcn_wave_barrier();
-        win[sel ? ((base + s) & WM) : W + j] = v;
-        emap[sel ? (v & MM) : kGMap + j] = make_int2(v, base + s);
+        win[sel ? ws : W + j] = v;
+        emap[sel ? (v & MM) : kGMap + j] = (uint8_t)ws;
         __builtin_amdgcn_wave_barrier();
       };
       chunk(0);
-      if (__builtin_amdgcn_ballot_w64(act && len >= 16))
-        for (int32_t c = 16; __builtin_amdgcn_ballot_w64(act && c <= len); c += 16) chunk(c);
+      if (actm & m_ge(len, 16))
+        for (int32_t c = 16; actm & m_le(c, len); c += 16) chunk(c);
   };
   // 16 pairs at a time: inverse LP of the raw words (x = prefix(prefix(y)) of the
   // sign-extended int32 sections, mod 2^64, decode :1004-1014 + :157-168; the sim uses the
@@ -795,7 +834,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
       // an id outside [0, M) among the batch's pairs fails the unit (for this tier) at once
       const bool inb = k0 + j >= ka && k0 + j < ke;
       const uint64_t badm = __builtin_amdgcn_ballot_w64(inb && (uint32_t)xs >= (uint32_t)M);
-      failv |= ((badm >> (threadIdx.x & 48)) & 0xffffu) ? 1 : 0;
+      failm |= m_ne((int32_t)((badm >> (threadIdx.x & 48)) & 0xffffu), 0);
     }
   };
   auto steps = [&](auto warm_c, int32_t k0, int32_t nq) {
@@ -804,7 +843,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
       const int32_t x = row_bcast<0>(xs), d = row_bcast<0>(ds);
       xs = __builtin_amdgcn_update_dpp(xs, xs, 0x101, 0xf, 0xf, false);  // row_shl:1
       ds = __builtin_amdgcn_update_dpp(ds, ds, 0x101, 0xf, 0xf, false);
-      step(warm_c, WARM ? wact : (k0 + q < ke), x, d);
+      step(warm_c, WARM ? wactm : m_lt(k0 + q, ke), x, d);
     }
   };
   // Two batches per round.  The raw words of a batch are loaded one batch ahead, and each
@@ -814,7 +853,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
   const std::integral_constant<bool, true> warm_t{};
   const std::integral_constant<bool, false> main_t{};
   int32_t ai, ad, bi, bd;
-  if (SEG && __builtin_amdgcn_ballot_w64(wact)) {
+  if (SEG && wactm) {
     const int32_t kb = ka - kSegWarm;  // (groups without a replay read nothing below ka: klo)
     ai = ld(yid, kb), ad = ld(ydl, kb), bi = ld(yid, kb + 16), bd = ld(ydl, kb + 16);
     for (int32_t i0 = 0; i0 < kSegWarm; i0 += 32) {
@@ -832,7 +871,6 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
       // before): that state is now also the one this segment is on record as having started from
       if (wact) {
         base = own;
-        for (int32_t q = j; q < kGMap; q += 16) emap[q] = make_int2(-1, -1);
         for (int32_t q = j; q < W; q += 16) {
           const int32_t v = dumpT[gi * W + q];
           dumpW[gi * W + q] = v;
@@ -841,12 +879,12 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
         __builtin_amdgcn_wave_barrier();
         for (int32_t q = j; q < W; q += 16) {
           const int32_t v = win[(own + q) & WM];
-          emap[v & MM] = make_int2(v, own + q);
+          emap[v & MM] = (uint8_t)((own + q) & WM);
         }
       }
     } else {
       // the window moves up to the first owned position; the state there goes to the check
-      while (__builtin_amdgcn_ballot_w64(wact && base < own)) slide(warm_t, wact && base < own);
+      for (mask64 gom; (gom = wactm & m_lt(base, own)) != 0;) slide(warm_t, gom);
       if (wact)
         for (int32_t q = j; q < W; q += 16) dumpW[gi * W + q] = win[(base + q) & WM];
     }
@@ -869,7 +907,7 @@ __global__ void __launch_bounds__(64) k_dec_perm_seg(DUnit* __restrict__ units, 
       steps(main_t, ka + i0 + 16, min(16, imax - i0 - 16));
     }
   }
-  const bool fail = failv != 0;
+  const bool fail = lane_of(failm);
   if (sim && fail && j == 0) {
     if (atomicCAS(&units[ui].fb, want_fb, want_fb + 1) == want_fb) atomicAdd(nfail, 1);
     if (SEG) atomicAdd(nfail + 4, 1);  // (diagnostics: segment runs that did not finish)
