@@ -2,7 +2,7 @@
 """CDC encode+decode throughput on MI355X (BASELINE.json metric).
 
 Workload (configs 3/4 of BASELINE.json): synthetic traces of a 1024-rank job, 10M events per
-rank (gen.h / DESIGN.md "Synthetic traces"): 327.7 GB of records, more than one GPU's HBM.
+rank (rempi_amd/csrc/gen.h): 327.7 GB of records, more than one GPU's HBM.
 The job's ranks are sharded over the GPUs in contiguous blocks (rank r -> GPU floor(r G / R),
 rempi_amd/shard.py); each GPU process walks its block in batches of at most --ranks-per-gpu
 rank traces resident in HBM.  Per batch: the traces are generated on the device (untimed),
@@ -488,7 +488,7 @@ def main():
         solo = {k: v for k, v in ln.ctx.kernel_times().items() if v[1] > 0}
         solo_records = ln.records
 
-    # Copy-inclusive rate (host memory in and out, DESIGN.md §6); never `value`.
+    # Copy-inclusive rate (host memory in and out); never `value`.
     host_io = None
     if args.host_io and rank == 0 and active:
         pins = []
@@ -653,7 +653,7 @@ def main():
         dist.destroy_process_group()
 
 
-# Algorithmic HBM bytes per input record for each kernel (DESIGN.md §3 kernel tables), from the
+# Algorithmic HBM bytes per input record for each kernel, from the
 # run's own mix: m = matched events per record, p = (id, delay) pairs per matched event, c =
 # compressed bytes per record.  The dominant kernel's figure is the roofline numerator.
 class Mix:

@@ -4,7 +4,7 @@
  * Plain C: pointers, sizes and int status codes only.  Each entry point names the
  * reference interface it replaces (paths relative to PRUNERS/ReMPI src/rempi/).
  *
- * Byte format: identical to rempi_encoder_cdc with REMPI_GZIP=0 (SURVEY.md §8(a) A5-A13):
+ * Byte format: identical to rempi_encoder_cdc with REMPI_GZIP=0:
  *   rank file = ( [size_t payload_len][payload] )* [size_t 0][footer]
  *   payload   = per matching-set table, ascending set id: int32 set_id, int32 count,
  *               size_t epoch bytes, size_t ranks[], size_t clocks[], size_t wp_len,
@@ -20,6 +20,9 @@
  *   [0] event_count [1] type [2] flag [3] rank [4] with_next [5] index [6] clock
  *   [7] matching_set_id
  * as rempi_event_list::push leaves them (consecutive duplicates already merged).
+ * Decoded records (what the files let a replay rebuild, per table in observed order): a matched
+ * event comes back as {1, 2, 1, rank, with_next != 0, index, clock, set id}, a run of unmatched
+ * polls as {event_count summed over the run, 2, 0, 0, 0, 0, 0, set id}.
  * Implementation limit: 0 <= matching_set_id < 256 (REMPI_MAX_RECV_TEST_ID is 128).
  */
 #ifndef CDCX_H
@@ -81,7 +84,7 @@ const char* cdcx_kernel_name(int k);
 int cdcx_encode_stream(cdcx_ctx* ctx, const int32_t* rec8, size_t n_rec, uint8_t** out,
                        size_t* out_len);
 
-/* REMPI_GZIP=1 stage of a whole rank file, on the host (SURVEY.md §8(f) 3): every chunk
+/* REMPI_GZIP=1 stage of a whole rank file, on the host: every chunk
  * payload replaced by its zlib stream (rempi_encoder_cdc::write_record_file,
  * rempi_encoder_cdc.cpp:804-844, deflate at Z_DEFAULT_COMPRESSION as in
  * rempi_compression_util.cpp:233-325) or back (read_record_file, :960-978); the separator
@@ -90,7 +93,7 @@ int cdcx_encode_stream(cdcx_ctx* ctx, const int32_t* rec8, size_t n_rec, uint8_t
 int cdcx_gzip_file(const uint8_t* in, size_t len, uint8_t** out, size_t* out_len);
 int cdcx_gunzip_file(const uint8_t* in, size_t len, uint8_t** out, size_t* out_len);
 
-/* Basic -> CDC transcoder (SURVEY.md §8(f) 2).  A REMPI_ENCODE=0 record file holds one
+/* Basic -> CDC transcoder.  A REMPI_ENCODE=0 record file holds one
  * rank's canonical event stream as [size_t len][len bytes of 8 x int32 events] chunks
  * (rempi_encoder_basic::write_record_file, rempi_encoder_basic.cpp:205-224; read back by
  * :238-321), so its CDC image is cdcx_encode_stream of the concatenated chunks.  The n_files
@@ -140,8 +143,8 @@ int cdcx_decode_stream(cdcx_ctx* ctx, const uint8_t* in, size_t len, uint8_t** d
                        size_t* dump_len);
 
 /* Host buffers: decode a rank file and rebuild each table's observed stream of canonical
- * records (SURVEY §8(a) decoded-record definition ii).  sorted_keys: per unit, file order,
- * the clock-sorted {source, clock} pairs.  *rec8 (cdcx_free) gets n_out x 8 int32. */
+ * records (the fields a replay can rebuild: see cdcx_reconstruct_chunk).  sorted_keys: per
+ * unit, file order, the clock-sorted {source, clock} pairs.  *rec8 (cdcx_free) gets n_out x 8 int32. */
 int cdcx_reconstruct_stream(cdcx_ctx* ctx, const uint8_t* in, size_t len,
                             const int32_t* sorted_keys, size_t n_keys, int32_t** rec8,
                             size_t* n_out);
@@ -182,8 +185,8 @@ typedef struct cdcx_tables {
  * of bounds. */
 int cdcx_decode_chunk(cdcx_ctx* ctx, const uint8_t* payload, size_t len, cdcx_tables* out);
 
-/* Host buffers: records reconstruction of ONE chunk payload (decoded-record definition ii,
- * the consumer side being cdc_decode_ordering :1655-1879): sorted_keys are the clock-sorted
+/* Host buffers: records reconstruction of ONE chunk payload (decoded records as defined
+ * above, the consumer side being cdc_decode_ordering :1655-1879): sorted_keys are the clock-sorted
  * {source, clock} pairs of the chunk's tables in ascending set id.  *rec8 (cdcx_free) gets
  * n_out x 8 int32. */
 int cdcx_reconstruct_chunk(cdcx_ctx* ctx, const uint8_t* payload, size_t len, const int32_t* sorted_keys,
@@ -244,13 +247,13 @@ int cdcx_decode_rank_offsets(cdcx_ctx* ctx, int32_t n_ranks, int64_t* rec_off, i
  * rempi_recorder.cpp:47-79).  Call right after cdcx_encode_batch_device(d_rec, ...) followed by
  * cdcx_decode_batch_device of its files with its sorted keys on the same context: every
  * decoded record is compared with the input record it must reproduce (per chunk, per table,
- * observed order; decoded-record definition ii).  *mismatches = records that differ.
+ * observed order; decoded records as defined above).  *mismatches = records that differ.
  * CDCX_ERR_ARG when the trace merges consecutive polls of one table (records are then not
  * 1:1; the synthetic workload never does). */
 int cdcx_verify_roundtrip_device(cdcx_ctx* ctx, const int32_t* d_rec, int64_t* mismatches, void* stream);
 
 /* ---------------------------------------------------------------------------------------
- * Replay-side streaming decode (config 5).  Replaces one
+ * Replay-side streaming decode of a whole record directory.  Replaces one
  * read_record_file (:933-978) + decode (:1016-1299) + cdc_prepare_decode_indices
  * (:1301-1386) loop per rank process, which progress_decoding (:851-930) runs over
  * REMPI_DIR/rank_<r>.rempi, by one pass over many rank files.
@@ -337,7 +340,7 @@ int cdcx_replay_decode_tables_ex(cdcx_ctx* const* ctxs, int32_t n_ctx, int32_t n
                                  void* user, cdcx_replay_stats* stats);
 
 /* ---------------------------------------------------------------------------------------
- * Synthetic workload (definition in DESIGN.md "Synthetic traces"), generated
+ * Synthetic workload (definition in rempi_amd/csrc/gen.h), generated
  * directly in device memory: n_ranks consecutive ranks starting at first_rank of a job of
  * world_size ranks, ~events_per_rank records each.  *d_rec (context-owned) and rec_off
  * (host, [n_ranks+1]) describe the result.  Also available on the host for tests. */

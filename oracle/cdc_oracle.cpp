@@ -1,7 +1,7 @@
 // oracle/cdc_oracle.cpp -- TEST INFRASTRUCTURE ONLY (see cdc_oracle.h).
 //
 // A deliberately plain, sequential CPU restatement of the reference CDC codec, written from
-// the behaviour spec rather than translated from the reference classes.
+// a written behaviour spec rather than translated from the reference classes.
 // Every function cites the reference code whose observable behaviour it reproduces
 // (paths relative to /root/reference/src/rempi).  Pinned by tests/test_oracle_golden.py
 // against bytes and tables produced by the reference itself (oracle/_ref/ref_cdc).

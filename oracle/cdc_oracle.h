@@ -1,7 +1,7 @@
 /* oracle/cdc_oracle.h -- TEST INFRASTRUCTURE ONLY.
  *
  * CPU restatement of the reference ReMPI Clock Delta Compression (CDC) codec, written
- * from the behaviour spec in SURVEY.md §8(a) (rows A1-A15) and pinned against the
+ * from a written behaviour spec of the reference's CDC path and pinned against the
  * reference's own encoder/decoder (oracle/_ref/ref_cdc, built from the unmodified
  * sources by oracle/Makefile) and the committed golden fixtures in tests/golden/.
  *
@@ -61,7 +61,7 @@ int64_t oracle_umap_order(const int64_t* keys, int64_t n, int64_t* out);
 /* Same for std::unordered_set<int> (the footer's all_epoch_rank_uset). */
 int64_t oracle_uset_int_order(const int32_t* keys, int64_t n, int32_t* out);
 
-/* Events-level decode for records parity (SURVEY §8(a) "decoded-record definition" ii):
+/* Events-level decode for records parity (the fields a replay can rebuild):
  * for every unit (chunk, table) of the file, rebuild the table's observed stream of
  * 32-B canonical records, given the unit's clock-sorted (source, clock) keys.
  * keys: concatenation over units (file order) of M_u pairs {source, clock} int32.

@@ -16,7 +16,7 @@
 //        the same push, then the REMPI_ENCODE=0 record loop with rempi_encoder_basic
 //        (rempi_encoder_basic.cpp:81-224): a sequence of [size_t len][len bytes of 8 x int32
 //        events] chunks (with `gzip`, REMPI_GZIP=1: each payload a zlib stream).  These files
-//        are what the basic -> CDC transcoder reads (§8(f)).
+//        are what the basic -> CDC transcoder reads.
 //   ref_cdc decode <in.rempi> <out.tables> [gzip]
 //        (`gzip`: REMPI_GZIP=1, chunk payloads are zlib streams)
 //        read_record_file + decode per chunk (rempi_encoder_cdc.cpp:933-1299), dumping the

@@ -1850,7 +1850,7 @@ int cdcx_verify_roundtrip_device(cdcx_ctx* c, const int32_t* d_rec, int64_t* mis
   });
 }
 
-// Replay-side streaming decode (SURVEY.md §8(f) 1): one host thread per context, each
+// Replay-side streaming decode: one host thread per context, each
 // taking whole batches of consecutive rank files off a shared counter.
 }  // extern "C"
 

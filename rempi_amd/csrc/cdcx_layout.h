@@ -1,6 +1,6 @@
 // cdcx_layout.h -- descriptors shared by the host orchestrator and the kernels.
 //
-// Vocabulary (SURVEY.md §8):
+// Vocabulary:
 //   rank   one process's record stream (one rank_<r>.rempi file)
 //   chunk  one extract_encoder_input_format_chunk epoch (<= REMPI_MAX length units)
 //   table  one matching set inside a chunk

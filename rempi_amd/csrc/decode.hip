@@ -1,4 +1,4 @@
-// decode.hip -- CDC replay-side kernels for gfx950 (SURVEY.md §8(a) A13-A16).
+// decode.hip -- CDC replay-side kernels for gfx950.
 //
 //   framing walk (read_record_file :933-978) -> unit section table (decode :1044-1200)
 //   -> inverse linear prediction of with_previous / unmatched ids / ids / delays as two
@@ -995,7 +995,7 @@ __global__ void __launch_bounds__(256) k_dec_cinv(const DUnit* __restrict__ unit
   for (int32_t v = threadIdx.x; v < u.M; v += 256) cinv[u.key_off + perm[u.key_off + v]] = v;
 }
 
-// Records reconstruction (decoded-record definition ii), one block per 1024-row tile of a
+// Records reconstruction (decoded records as include/cdcx.h defines them), one block per 1024-row tile of a
 // unit: matched row i is the event of clock order c_i (cinv, written by the permutation
 // rebuild) with the replay-supplied sorted key; with_next from the row flags, index from
 // matched_index; unmatched run k with id `id` sits right before matched row `id`, so row

@@ -1,6 +1,6 @@
 // encode.hip -- CDC record-side kernels for gfx950.
 //
-// Pipeline (one batch = many independent rank streams, SURVEY.md §8(a) A2-A12):
+// Pipeline (one batch = many independent rank streams):
 //   set discovery -> stable partition by table (T-order) -> length increments + prefix
 //   -> chunk boundaries (A3) -> units -> per-unit compaction (A3 add) -> tile sort + merge
 //   rank = clock order (A4) -> epoch line in libstdc++ hash order (A4) -> chain (A7)

@@ -1,6 +1,6 @@
-// gen.h -- the synthetic per-rank MPI event traces of SURVEY.md §8(d), defined as closed-form
+// gen.h -- the synthetic per-rank MPI event traces of the benchmark workload, defined as closed-form
 // functions of (rank, index) so that the host (tests, CPU baseline) and the device (bench)
-// produce bit-identical streams.  Definition, in words (DESIGN.md "Synthetic traces"):
+// produce bit-identical streams.  Definition, in words:
 //
 //  * A rank r of a job of W ranks has S' = min(S, W-1) senders; sender j sends from rank
 //    (r + 1 + j) mod W and belongs to matching set t = j mod T' (T' = min(T, S')).

@@ -1,4 +1,4 @@
-// gzip_stage.hip -- the REMPI_GZIP=1 stage of a CDC rank file, on the host (SURVEY.md §8(f) 3).
+// gzip_stage.hip -- the REMPI_GZIP=1 stage of a CDC rank file, on the host.
 //
 // With REMPI_GZIP=1 the reference writes each chunk as [size_t compressed size][one zlib stream
 // of the chunk payload] (rempi_encoder_cdc::write_record_file, rempi_encoder_cdc.cpp:804-844;

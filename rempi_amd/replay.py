@@ -1,4 +1,4 @@
-"""Replay-side streaming decode of a REMPI_DIR (BASELINE config 5).
+"""Replay-side streaming decode of a REMPI_DIR (the benchmark's config 5).
 
 In the reference every replaying rank process runs progress_decoding
 (rempi_encoder_cdc.cpp:851-930): read_record_file (:933-978) -> decode (:1016-1299) ->

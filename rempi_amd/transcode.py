@@ -1,4 +1,4 @@
-"""Basic -> CDC transcoder (SURVEY.md §8(f) 2): shrink existing REMPI_ENCODE=0 record files.
+"""Basic -> CDC transcoder: shrink existing REMPI_ENCODE=0 record files.
 
     python -m rempi_amd.transcode [--max-len REMPI_MAX] [--batch 16] -o OUTDIR rank_*.rempi
 

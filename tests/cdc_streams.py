@@ -102,7 +102,7 @@ def gen_stream(seed: int, n_matched: int, n_sets: int = 2, n_senders: int = 8, j
 
 def kat_stream() -> np.ndarray:
     """Known-answer input of test/rempi/rempi_test_compress.cpp:104-113 (rank 1, clocks
-    32,11,17,36,31,12,22,10,16,18) framed as in SURVEY §8(c): 5 polls, the 10 matched
+    32,11,17,36,31,12,22,10,16,18) framed as a recorder would: 5 polls, the 10 matched
     receives, 3 polls (already run-length merged)."""
     recs = [[5, TEST, 0, 0, 0, 0, 0, 0]]
     for c in [32, 11, 17, 36, 31, 12, 22, 10, 16, 18]:
@@ -146,7 +146,7 @@ def chunk_bounds(recs: np.ndarray, max_len: int):
 
 
 def expected_table_streams(recs: np.ndarray, max_len: int) -> np.ndarray:
-    """Decoded-record parity target (definition ii): per chunk, per table in
+    """Decoded-record parity target: per chunk, per table in
     ascending set id, the table's records in observed order as the decoder can rebuild them
     -- consecutive unmatched polls of a table merged (counts summed, add() :205-208),
     unmatched fields other than count/type/set zeroed, with_next normalised to 0/1, matched

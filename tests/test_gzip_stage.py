@@ -1,4 +1,4 @@
-"""REMPI_GZIP=1 stage (SURVEY.md §8(f) 3): host zlib over the GPU's CDC chunks must give the
+"""REMPI_GZIP=1 stage: host zlib over the GPU's CDC chunks must give the
 reference's own REMPI_GZIP=1 files byte for byte (fixtures written by the reference encoder,
 tests/golden/make_gzip_golden.py), and gzip contexts must encode / decode them."""
 import numpy as np

@@ -92,7 +92,7 @@ def test_oracle_records_roundtrip(name):
 
 
 def test_kat_values():
-    """Known answers of SURVEY §8(c) for rempi_test_compress.cpp:104-113."""
+    """Known answers for the permutation of rempi_test_compress.cpp:104-113."""
     data, _ = O.encode(S.kat_stream(), 131072)
     assert len(data) == 280
     t = O.parse_tables(O.decode(data))[0][0]

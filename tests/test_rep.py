@@ -1,4 +1,4 @@
-"""Rep encoder (REMPI_ENCODE=7, SURVEY.md §8(f) 4; rempi_encoder_rep.cpp:50-146): every
+"""Rep encoder (REMPI_ENCODE=7; rempi_encoder_rep.cpp:50-146): every
 table keeps its set id, matched count and epoch line; the with_previous, matched_index,
 unmatched and pair sections are written empty.  Fixtures are the reference's own rep files
 (tests/golden/make_rep_golden.py); rep files decode through the CDC decoder (the class

@@ -1,4 +1,4 @@
-"""Replay-side streaming decode (SURVEY.md §8(f) 1): cdcx_replay_decode_files over a
+"""Replay-side streaming decode: cdcx_replay_decode_files over a
 REMPI_DIR of rank files must hand every file's tables to the sink exactly as
 cdcx_decode_stream / the reference decode() produce them for that file alone, whatever
 the batching and the number of contexts.  Rank files are the reference-written golden

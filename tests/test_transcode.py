@@ -1,4 +1,4 @@
-"""Basic -> CDC transcoder (SURVEY.md §8(f) 2): REMPI_ENCODE=0 record files, written by the
+"""Basic -> CDC transcoder: REMPI_ENCODE=0 record files, written by the
 reference's own rempi_encoder_basic (fixtures from tests/golden/make_basic_golden.py), must
 come out as the reference CDC encoder's files for the same events.  CPU tests pin the file
 format and the claim (oracle); GPU tests run cdcx_transcode_basic."""

@@ -12,6 +12,6 @@ timeout -k 10 400 python -u bench.py --kernel-report > $OUT/bench.json 2> $OUT/b
 cat $OUT/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --max-batches 2 --cpu-baseline 0 --host-io 0 --solo 0 > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/prof.log; exit 1; }
 cp $OUT/prof/run_kernel_stats.csv $OUT/kernel_stats.csv
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_solo -o run --output-format csv -- python3 bench.py --streams 1 --ranks-per-gpu 24 --steps 3 --warmup 1 --max-batches 1 --cpu-baseline 0 --host-io 0 --solo 0 > $OUT/prof_solo.log 2>&1 || { echo "rocprof (one lane) failed"; tail -30 $OUT/prof_solo.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_solo -o run --output-format csv -- python3 bench.py --streams 1 --ranks-per-gpu 32 --steps 3 --warmup 1 --max-batches 1 --cpu-baseline 0 --host-io 0 --solo 0 > $OUT/prof_solo.log 2>&1 || { echo "rocprof (one lane) failed"; tail -30 $OUT/prof_solo.log; exit 1; }
 cp $OUT/prof_solo/run_kernel_stats.csv $OUT/solo_kernel_stats.csv
 head -8 $OUT/solo_kernel_stats.csv | cut -c1-200

@@ -1,10 +1,10 @@
-"""Config 5 measurement (SURVEY.md §8(f) 1): streaming replay decode of a REMPI_DIR.
+"""Config 5 measurement: streaming replay decode of a REMPI_DIR.
 
 Writes R synthetic rank files (the bench workload at E events/rank, CDC-encoded on the GPU)
 into a directory, then decodes the whole directory with rempi_amd.replay (file read ->
 pinned host buffer -> H2D -> decode kernels -> D2H of the tables -> per-rank table dumps),
 and prints one JSON line.  Under torchrun each process takes the ranks r with
-r * WORLD_SIZE // R == RANK (contiguous blocks); no collective.
+r * WORLD_SIZE // R == RANK (contiguous blocks, as rempi_amd/shard.py); no collective.
 
     python tools/replay_bench.py --ranks 4096 --events 100000 --dir /tmp/rempi_dir
 """
