@@ -247,9 +247,8 @@ int cdcx_decode_rank_offsets(cdcx_ctx* ctx, int32_t n_ranks, int64_t* rec_off, i
  * rempi_recorder.cpp:47-79).  Call right after cdcx_encode_batch_device(d_rec, ...) followed by
  * cdcx_decode_batch_device of its files with its sorted keys on the same context: every
  * decoded record is compared with the input record it must reproduce (per chunk, per table,
- * observed order; decoded records as defined above).  *mismatches = records that differ.
- * CDCX_ERR_ARG when the trace merges consecutive polls of one table (records are then not
- * 1:1; the synthetic workload never does). */
+ * observed order; decoded records as defined above: a run of polls that the encoder merged
+ * is one record with the summed count).  *mismatches = decoded records that differ. */
 int cdcx_verify_roundtrip_device(cdcx_ctx* ctx, const int32_t* d_rec, int64_t* mismatches, void* stream);
 
 /* ---------------------------------------------------------------------------------------

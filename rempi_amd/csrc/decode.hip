@@ -1053,30 +1053,64 @@ __global__ void __launch_bounds__(256) k_dec_records(const DUnit* __restrict__ u
 }
 
 // Round-trip check on the device: record i of encoder unit u's T-order range is input record
-// rec_off[rank] + t2s[a + i]; after encode + decode of the same batch it must reappear as
-// decoded record dec_off[u] + i with the fields the replay side can rebuild (matched:
-// count 1, type 2, flag 1, source, with_next as 0/1, index, clock, set; unmatched poll: count,
-// type 2, set, everything else 0).  Holds when no two polls of a table were merged
-// (M + U == n for every unit); the host checks that before launching.
+// rec_off[rank] + the stream position kept in its T-order record; after encode + decode of the
+// same batch the unit's decoded records (dec_off[u] on) must be the fields the replay side can
+// rebuild, in the same order: a matched event as {1, 2, 1, source, with_next as 0/1, index,
+// clock, set}, and every maximal run of unmatched polls as ONE record {sum of the run's counts,
+// 2, 0, 0, 0, 0, 0, set} (the encoder merges the polls before a matched event into one run).
+// Input record i therefore lands at decoded index #(matched events and run starts before i);
+// the thread of a run's first poll adds up the run.
 __global__ void __launch_bounds__(256) k_verify_roundtrip(const Unit* __restrict__ units, const int64_t* __restrict__ dec_off,
                                                           const int64_t* __restrict__ rec_off,
                                                           const TRec* __restrict__ trec, const int4* __restrict__ rec_in,
                                                           const int4* __restrict__ rec_out,
                                                           unsigned long long* __restrict__ bad) {
+  __shared__ int32_t lds[4];
   const Unit u = units[blockIdx.x];
   const int64_t rb = rec_off[u.rank], ob = dec_off[blockIdx.x];
-  int32_t nbad = 0;
-  for (int32_t i = threadIdx.x; i < u.n; i += 256) {
-    const int64_t g = rb + (int64_t)(trec[u.a + i].info & kInfoPos);
-    const int4 lo = rec_in[2 * g], hi = rec_in[2 * g + 1];
-    const int4 a = rec_out[2 * (ob + i)], b = rec_out[2 * (ob + i) + 1];
-    const bool m = lo.z == 1;
-    const int4 wa = m ? make_int4(1, 2, 1, lo.w) : make_int4(lo.x, 2, 0, 0);
-    const int4 wb = m ? make_int4(hi.x != 0 ? 1 : 0, hi.y, hi.z, hi.w) : make_int4(0, 0, 0, hi.w);
+  const int64_t n_out = dec_off[blockIdx.x + 1] - ob;
+  auto in_rec = [&](int32_t i) { return rb + (int64_t)(trec[u.a + i].info & kInfoPos); };
+  int32_t nbad = 0, carry = 0;
+  for (int32_t i0 = 0; i0 < u.n; i0 += 256) {
+    const int32_t i = i0 + threadIdx.x;
+    const bool ok = i < u.n;
+    int4 lo = make_int4(0, 0, 0, 0), hi = lo;
+    bool m = false, emits = false;
+    if (ok) {
+      const int64_t g = in_rec(i);
+      lo = rec_in[2 * g];
+      hi = rec_in[2 * g + 1];
+      m = lo.z == 1;
+      emits = m || i == 0 || rec_in[2 * in_rec(i - 1)].z == 1;  // a matched event, or the first poll of a run
+    }
+    int32_t tot;
+    const int32_t at = carry + block_exclusive_scan<256>(emits ? 1 : 0, 0, OpAdd(), lds, &tot);
+    carry += tot;
+    if (!emits) continue;
+    if (at >= n_out) {
+      nbad++;
+      continue;
+    }
+    int4 wa, wb;
+    if (m) {
+      wa = make_int4(1, 2, 1, lo.w);
+      wb = make_int4(hi.x != 0 ? 1 : 0, hi.y, hi.z, hi.w);
+    } else {
+      int32_t cnt = lo.x;
+      for (int32_t k = i + 1; k < u.n; k++) {
+        const int4 q = rec_in[2 * in_rec(k)];
+        if (q.z == 1) break;
+        cnt += q.x;
+      }
+      wa = make_int4(cnt, 2, 0, 0);
+      wb = make_int4(0, 0, 0, hi.w);
+    }
+    const int4 a = rec_out[2 * (ob + at)], b = rec_out[2 * (ob + at) + 1];
     if (a.x != wa.x || a.y != wa.y || a.z != wa.z || a.w != wa.w || b.x != wb.x || b.y != wb.y || b.z != wb.z ||
         b.w != wb.w)
       nbad++;
   }
+  if (threadIdx.x == 0 && carry != n_out) nbad++;  // (records the decode has and the input does not account for)
   nbad = wave_reduce(nbad, OpAdd());
   if (lane_id() == 0 && nbad) atomicAdd(bad, (unsigned long long)nbad);
 }

@@ -142,6 +142,51 @@ def test_batch_encode_decode_vs_oracle(batch):
     np.testing.assert_array_equal(recs, want)
 
 
+def test_verify_roundtrip_with_merged_poll_runs():
+    """cdcx_verify_roundtrip_device on traces whose tables merge polls into runs (polls of one
+    table that other tables' events separate in the stream): the decoded records are fewer than
+    the input records, every run is one record with the summed count, and the check finds a
+    single changed word on either side."""
+    traces = []
+    for seed in (11, 12, 13):
+        rng = np.random.default_rng(seed)
+        t = S.gen_stream(seed, 2500, n_sets=3, n_senders=6, jitter=8, p_unmatched=0.5, p_group=0.1)
+        # extra polls of a table between other tables' records: next to that table's own polls in its stream
+        rows = []
+        for r in t:
+            rows.append(r)
+            if r[4] == 0 and rng.random() < 0.3:
+                rows.append(np.array([1 + int(rng.integers(7)), 2, 0, 0, 0, 0, 0, (int(r[7]) + 1 + int(rng.integers(2))) % 3], np.int32))
+        traces.append(S.canonicalize(np.array(rows, np.int32)))
+    rec_off = np.concatenate([[0], np.cumsum([t.shape[0] for t in traces])]).astype(np.int64)
+    mx = 700
+    dev = cdcx.DeviceArray(np.concatenate(traces))
+    c = ctx(mx)
+    try:
+        d_out, off, ln = c.encode_batch_device(dev.ptr, rec_off)
+        d_keys, n_keys = c.batch_sorted_keys()
+        d_recs, n_recs, _ = c.decode_batch_device(d_out, off, ln, d_keys, n_keys)
+        want = np.concatenate([S.expected_table_streams(t, mx) for t in traces])
+        assert n_recs == want.shape[0] < rec_off[-1]  # runs were merged
+        np.testing.assert_array_equal(cdcx.d2h(d_recs, n_recs * 32, np.int32).reshape(-1, 8), want)
+        assert c.verify_roundtrip_device(dev.ptr) == 0
+        # a run's count on the decoded side, then a poll's count on the input side
+        k = int(np.flatnonzero((want[:, 2] == 0) & (want[:, 0] > 1))[0])
+        word = np.array([want[k, 0] + 1], np.int32)
+        assert cdcx.hip().hipMemcpy(d_recs + 32 * k, word.ctypes.data, 4, 1) == 0
+        assert c.verify_roundtrip_device(dev.ptr) == 1
+        word[0] = want[k, 0]
+        assert cdcx.hip().hipMemcpy(d_recs + 32 * k, word.ctypes.data, 4, 1) == 0
+        assert c.verify_roundtrip_device(dev.ptr) == 0
+        allr = np.concatenate(traces)
+        j = int(np.flatnonzero(allr[:, 2] == 0)[5])
+        word[0] = allr[j, 0] + 3
+        assert cdcx.hip().hipMemcpy(dev.ptr + 32 * j, word.ctypes.data, 4, 1) == 0
+        assert c.verify_roundtrip_device(dev.ptr) == 1
+    finally:
+        dev.close()
+
+
 @pytest.mark.parametrize("jitter,world,events,max_len", [(0, 64, 40000, 131072), (32, 256, 120000, 131072),
                                                           (128, 1024, 60000, 8192), (8, 4, 30000, 512)])
 def test_generator_workloads_vs_oracle(jitter, world, events, max_len):
