@@ -143,6 +143,28 @@ constexpr int kGateKinds = 3;
 constexpr int kGateDevices = 16;
 static Gate g_gates[kGateDevices][kGateKinds];
 
+// Library calls in flight per device (guarded()).  The chain kernel is a work queue whose grid
+// decides how much of every CU it holds for its ten-odd milliseconds: five blocks per CU (1280)
+// make it fastest alone; beside other contexts' kernels 3.5 per CU (896) leave them the LDS and
+// wave slots they are short of, and the step of four lanes is 3 % shorter.
+static std::atomic<int> g_calls_in_flight[kGateDevices];
+struct InFlight {
+  int d;
+  explicit InFlight(int dev) : d(dev) {
+    if (d >= 0 && d < kGateDevices) g_calls_in_flight[d].fetch_add(1, std::memory_order_relaxed);
+  }
+  ~InFlight() {
+    if (d >= 0 && d < kGateDevices) g_calls_in_flight[d].fetch_sub(1, std::memory_order_relaxed);
+  }
+  InFlight(const InFlight&) = delete;
+  InFlight& operator=(const InFlight&) = delete;
+};
+inline int64_t chain_blocks(int64_t forced, int device) {
+  if (forced > 0) return forced;
+  const bool shared = device >= 0 && device < kGateDevices && g_calls_in_flight[device].load(std::memory_order_relaxed) > 1;
+  return shared ? 896 : 1280;
+}
+
 struct cdcx_ctx {
   int device = 0;
   unsigned char* static_scratch = nullptr;  // this device's `scratch` (static_scratch_of)
@@ -203,9 +225,8 @@ struct cdcx_ctx {
   int dec_tier = getenv("CDCX_DEC_TIER") ? atoi(getenv("CDCX_DEC_TIER")) : 0;
   // 1: every unit takes the tile sort (skips the windowed rank), for tests
   int rank_tier = getenv("CDCX_RANK_TIER") ? atoi(getenv("CDCX_RANK_TIER")) : 0;
-  // blocks of the first chain tier (a work queue).  896 = 3.5 blocks per CU: with four lanes in flight the
-  // step is 3 % shorter than with 1280 (five per CU), which the kernel alone does not need to stay issue-bound
-  int64_t chain_grid = getenv("CDCX_CHAIN_GRID") ? std::max(1, atoi(getenv("CDCX_CHAIN_GRID"))) : 896;
+  // blocks of the first chain tier (a work queue); 0 = by what else runs on the device (chain_blocks())
+  int64_t chain_grid = getenv("CDCX_CHAIN_GRID") ? std::max(1, atoi(getenv("CDCX_CHAIN_GRID"))) : 0;
   bool chain_g16 = getenv("CDCX_CHAIN_G16") != nullptr;  // first tier on 16-lane groups (A/B timing)
   // segments of at least this many events run at raised wave priority in the 8-lane chain tier
   int chain_long = getenv("CDCX_CHAIN_LONG") ? atoi(getenv("CDCX_CHAIN_LONG")) : 1536;
@@ -362,6 +383,7 @@ int guarded(cdcx_ctx* c, F&& f) {
   if (!c) return CDCX_ERR_ARG;
   try {
     HIPCHK(hipSetDevice(c->device));
+    InFlight in_flight(c->device);
     f();
     c->err.clear();
     return CDCX_OK;
@@ -710,12 +732,12 @@ void encode_batch(cdcx_ctx* c, int32_t R, const int32_t* d_rec, const int64_t* r
       // (the 8-lane kernel addresses rows by 32-bit byte offsets)
       if (c->chain_g16 || N >= (int64_t(1) << 30))
         c->launch(K_CHAIN_G16, k_chain_grp<16>,
-                  dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(c->chain_grid, blocks(n, 64)))), dim3(256), s,
+                  dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(chain_blocks(c->chain_grid, c->device), blocks(n, 64)))), dim3(256), s,
                   (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,
                   d_topg, d_qn, d_ovf1, d_cnt + 1, d_err);
       else
         c->launch_gated(0, n >= 65536, K_CHAIN_G8, k_chain_grp8,
-                  dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(c->chain_grid, blocks(n, 128)))), dim3(256), s,
+                  dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(chain_blocks(c->chain_grid, c->device), blocks(n, 128)))), dim3(256), s,
                   (const Unit*)d_units, d_segs, list, nlist, (const int32_t*)d_cord, (const int32_t*)d_opn, d_par, d_exta,
                   d_topg, d_qn, d_ovf1, d_cnt + 1, (int32_t)c->chain_long, d_err);
       list = d_ovf1;
