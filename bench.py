@@ -57,7 +57,7 @@ def parse(argv=None):
     ap.add_argument("--ranks-per-gpu", type=int, default=128, help="rank traces resident per GPU (one batch)")
     ap.add_argument("--jitter", type=int, default=8)
     ap.add_argument("--max-len", type=int, default=131072, help="REMPI_MAX")
-    ap.add_argument("--streams", type=int, default=4, help="lanes of a batch in flight per GPU (one HIP stream each)")
+    ap.add_argument("--streams", type=int, default=8, help="lanes of a batch in flight per GPU (one HIP stream each)")
     ap.add_argument("--max-batches", type=int, default=0,
                     help="process only the first B batches of each GPU's block (0 = the whole block)")
     ap.add_argument("--verify", type=int, default=1, help="verify every rank after the timed steps of its batch")
@@ -68,11 +68,14 @@ def parse(argv=None):
     ap.add_argument("--cpu-workers", type=int, default=0, help="CPU worker processes (0 = the cores this process may use)")
     ap.add_argument("--kernel-report", action="store_true", help="print per-kernel times to stderr")
     ap.add_argument("--host-io", type=int, default=1, help="steps of the copy-inclusive measurement (0 = skip)")
-    ap.add_argument("--host-io-ranks", type=int, default=12, help="rank traces per lane in the copy-inclusive measurement")
+    ap.add_argument("--host-io-ranks", type=int, default=12, help="rank traces per lane (of at most four) in the copy-inclusive measurement")
     ap.add_argument("--config2", type=int, default=-1,
                     help="also run config 2 (the CPU sample's 64 x 1M traces) on the GPU and compare its files with the CPU "
                          "codec's (default: when the CPU baseline runs)")
     ap.add_argument("--solo", type=int, default=2, help="steps of one lane alone for the roofline figure (0 = skip)")
+    ap.add_argument("--solo-ranks", type=int, default=32,
+                    help="rank traces of that launch: enough to keep the GPU full for the whole kernel (a lane of the timed "
+                         "steps holds ranks-per-gpu / streams, whose chain kernel alone ends in the tail of its longest segments)")
     return ap.parse_args(argv)
 
 
@@ -344,7 +347,7 @@ def verify_lane(ln: Lane, fixture: dict, oracle_ranks=(), p=None, max_len=131072
 
 def run_config2(args, device, file_sha, steps=6):
     """Config 2 of BASELINE.json on the GPU, beside the CPU leg that runs it in full: the 64 rank
-    traces x 1M events of the same generator, one resident batch on --streams lanes, encoded and
+    traces x 1M events of the same generator, one resident batch on up to four lanes, encoded and
     decoded `steps` times (timed, device-resident), every rank verified by the device round trip,
     and every rank file compared (SHA-256) with the one the CPU codec wrote for that rank."""
     import torch
@@ -354,7 +357,7 @@ def run_config2(args, device, file_sha, steps=6):
 
     n = args.cpu_sample_ranks
     p = rempi_amd.default_gen_params(world_size=args.world, jitter=args.jitter, events_per_rank=args.cpu_sample_events)
-    lanes = [Lane(args.max_len, device) for _ in range(max(1, min(args.streams, n)))]
+    lanes = [Lane(args.max_len, device) for _ in range(max(1, min(args.streams, 4, n)))]  # (16 traces of 1 M events per lane)
     try:
         at = 0
         for ln, k in zip(lanes, shard.lane_sizes(n, len(lanes))):
@@ -392,6 +395,13 @@ def run_config2(args, device, file_sha, steps=6):
 def main():
     args = parse()
     ws, rank, local = dist_env()
+    # One hardware queue per lane: with HIP's default of 4 two lanes share a queue and run one behind
+    # the other (5 lanes on 4 queues are slower than 4).  Read when the HIP runtime starts, so set
+    # before anything touches the GPU.
+    want_q = min(16, max(4, args.streams))
+    have_q = os.environ.get("GPU_MAX_HW_QUEUES", "")
+    if not have_q.isdigit() or int(have_q) < want_q:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
     import torch
 
     # One process per GPU over RCCL.  CDCX_BENCH_BACKEND=gloo is the rehearsal of the N > 1 path
@@ -476,22 +486,14 @@ def main():
             ktimes[k] = (a0 + ms, b0 + nl)
         ln.ctx.reset_kernel_times()
 
-    # Dominant kernel alone on the GPU (one lane, nothing else in flight): its launch duration
-    # for the roofline figure.  Under --streams lanes the HIP events of a launch also cover the
-    # time the lane shares the CUs with the other lanes.
-    solo = {}
-    if args.solo and rank == 0 and active:
-        ln = active[0]
-        ln.ctx.set_profiling(True)
-        run_lanes([ln], Lane.step, args.solo)
-        ln.ctx.set_profiling(False)
-        solo = {k: v for k, v in ln.ctx.kernel_times().items() if v[1] > 0}
-        solo_records = ln.records
+    chain_tiers0 = lanes[0].ctx.chain_tiers()  # (of the timed steps: the legs below reload the lanes)
+    decode_tiers = [ln.ctx.decode_tiers() for ln in lanes]
 
     # Copy-inclusive rate (host memory in and out); never `value`.
     host_io = None
     if args.host_io and rank == 0 and active:
         pins = []
+        active = active[:4]  # (four lanes fill the PCIe link; more only split it)
         for ln in active:  # a bounded sample: 88 B of pinned host memory per record
             if ln.n > args.host_io_ranks:
                 ln.load(p, ln.first, args.host_io_ranks)
@@ -510,6 +512,27 @@ def main():
         for pr in pins:
             for b in pr:
                 b.close()
+
+    # Dominant kernel alone on the GPU (one lane, nothing else in flight): its launch duration
+    # for the roofline figure.  Under --streams lanes the HIP events of a launch also cover the
+    # time the lane shares the CUs with the other lanes.  The other lanes are closed first, so
+    # that the one lane can hold --solo-ranks traces.
+    solo = {}
+    if args.solo and rank == 0 and active:
+        for ln in lanes[1:]:
+            ln.close()
+        lanes = lanes[:1]
+        ln = lanes[0]
+        want = max(1, min(args.solo_ranks, args.ranks_per_gpu, count))
+        if ln.n != want:
+            ln.load(p, first, want)
+        run_lanes([ln], Lane.step, 1)
+        ln.ctx.reset_kernel_times()
+        ln.ctx.set_profiling(True)
+        run_lanes([ln], Lane.step, args.solo)
+        ln.ctx.set_profiling(False)
+        solo = {k: v for k, v in ln.ctx.kernel_times().items() if v[1] > 0}
+        solo_records = ln.records
 
     counters, tmax = shard.reduce_counters(
         [n_records * args.steps, comp_bytes, ver["enc_ranks"], ver["enc_fail"], ver["dec_ranks"], ver["dec_fail"],
@@ -568,12 +591,14 @@ def main():
             so = solo.get(k)
             print(f"  {k:22s} {ms / max(n, 1):10.3f} ms/launch x{n:5d}  {100 * ms / tot:5.1f}%"
                   + (f"   alone {so[0] / so[1]:8.3f} ms" if so else ""), file=sys.stderr)
+        if solo:
+            print(f"  (per launch: {per_launch_records} records with all lanes in flight, {solo_records} alone)", file=sys.stderr)
         print(f"  timed {elapsed:.3f}s for {args.steps} steps x {len(plan)} batches on {n_lanes} streams; "
               f"kernels sum {tot / 1e3:.3f}s; job wall {job_wall:.1f}s", file=sys.stderr)
         print(f"  chain tiers of the last encode of lane 0 (segments: all, past 16 leaves, past 64): "
-              f"{lanes[0].ctx.chain_tiers()}", file=sys.stderr)
+              f"{chain_tiers0}", file=sys.stderr)
         print(f"  rebuild tiers of the lanes' last decodes (tables: all, whole-table groups, window, list; segments: all, "
-              f"rerun, given up): {[ln.ctx.decode_tiers() for ln in lanes]}", file=sys.stderr)
+              f"rerun, given up): {decode_tiers}", file=sys.stderr)
         for note in ver["notes"][:20]:
             print("  verify:", note, file=sys.stderr)
 
@@ -610,7 +635,7 @@ def main():
                        "job_ranks": args.world, "ranks_processed": ranks_done, "batches_per_gpu": len(plan),
                        "ranks_per_batch": args.ranks_per_gpu, "events_per_rank": args.events,
                        "records_per_step": int(total_records / args.steps),
-                       "jitter": args.jitter, "rempi_max": args.max_len, "streams_per_gpu": n_lanes,
+                       "jitter": args.jitter, "rempi_max": args.max_len, "streams_per_gpu": n_lanes, "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "compressed_bytes_per_event": round(comp_per_event, 3),
                        "hbm_used_gb": round((total_b - free_b) / 1e9, 1), "hbm_total_gb": round(total_b / 1e9, 1),
                        "parallelism": f"dp{ws}: rank r -> GPU floor(r*{ws}/{args.world}), independent rank traces",
