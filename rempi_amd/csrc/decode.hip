@@ -1100,7 +1100,7 @@ __global__ void __launch_bounds__(256) k_verify_roundtrip(const Unit* __restrict
       for (int32_t k = i + 1; k < u.n; k++) {
         const int4 q = rec_in[2 * in_rec(k)];
         if (q.z == 1) break;
-        cnt += q.x;
+        cnt = (int32_t)((uint32_t)cnt + (uint32_t)q.x);  // (the encoder's sum wraps in 32 bits)
       }
       wa = make_int4(cnt, 2, 0, 0);
       wb = make_int4(0, 0, 0, hi.w);
