@@ -142,6 +142,51 @@ def test_batch_encode_decode_vs_oracle(batch):
     np.testing.assert_array_equal(recs, want)
 
 
+def test_eight_contexts_in_flight_vs_oracle():
+    """Eight contexts of one process, one host thread and HIP stream each, encoding and decoding
+    different rank traces at the same time (the bench's lanes): the gates, the per-device count of
+    calls in flight and the chain kernel's grid that follows it are shared state.  Every file and
+    every decoded record stream must be what the same call gives alone."""
+    import threading
+
+    p = rempi_amd.default_gen_params(world_size=64, events_per_rank=50000)
+    n_lanes, per_lane, rounds = 8, 2, 3
+    host = {r: rempi_amd.generate_host(p, r) for r in range(n_lanes * per_lane)}
+    want_file = {r: O.encode(h, 131072)[0] for r, h in host.items()}
+    want_recs = {r: S.expected_table_streams(h, 131072) for r, h in host.items()}
+    errs = []
+
+    def lane(k):
+        try:
+            c = ctx(131072)
+            s = cdcx.stream_create()
+            first = k * per_lane
+            d_rec, rec_off = c.generate_device(p, first, per_lane, stream=s)
+            for _ in range(rounds):
+                d_out, off, ln = c.encode_batch_device(d_rec, rec_off, stream=s)
+                d_keys, n_keys = c.batch_sorted_keys()
+                d_recs, n_recs, _ = c.decode_batch_device(d_out, off, ln, d_keys, n_keys, stream=s)
+                cdcx.stream_sync(s)
+                for q in range(per_lane):
+                    got = cdcx.d2h(d_out + int(off[q]), int(ln[q])).tobytes()
+                    if got != want_file[first + q]:
+                        errs.append((k, q, "file", first_diff(got, want_file[first + q])))
+                recs = cdcx.d2h(d_recs, n_recs * 32, np.int32).reshape(-1, 8)
+                if not np.array_equal(recs, np.concatenate([want_recs[first + q] for q in range(per_lane)])):
+                    errs.append((k, "records"))
+            cdcx.stream_destroy(s)
+            c.close()
+        except Exception as e:  # noqa: BLE001 - reported on the main thread
+            errs.append((k, repr(e)))
+
+    ts = [threading.Thread(target=lane, args=(k,)) for k in range(n_lanes)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs[:4]
+
+
 def test_verify_roundtrip_with_merged_poll_runs():
     """cdcx_verify_roundtrip_device on traces whose tables merge polls into runs (polls of one
     table that other tables' events separate in the stream): the decoded records are fewer than
